@@ -1,0 +1,221 @@
+/*
+ * mp2vg.h — C ABI of the MI355X-native MPEG-2 macroblock reconstruct path.
+ *
+ * Plain C, plain pointers and sizes, int status codes; no torch / HIP types in any signature.
+ * The shared library is tiny_mp2v_dec_amd/_build/libmp2vg.so (hipcc, gfx950).
+ *
+ * What each group of entry points replaces in the reference (fxslava/tiny_mp2v_dec):
+ *
+ *   mp2vg_create / mp2vg_destroy / mp2vg_frame_geometry
+ *       replace decoder_init's frame pool (reference src/core/decoder.cpp:381-406) and the
+ *       frame_c plane layout (decoder.h:34-49, decoder.cpp:44-77): 3 planes per picture,
+ *       stride = round_up(width, 64), chroma stride = round_up(stride/2, 64) (4:4:4: = stride).
+ *   mp2vg_batch_upload / mp2vg_batch_decode
+ *       replace the per-slice hot loop `do { m_parse_macroblock_func(&bs, cache); } while(...)`
+ *       (decoder.cpp:148-150) — i.e. everything parse_macroblock_template does AFTER parsing:
+ *       MC (mb_decoder.cpp:291-339 -> mc.cpp tables -> mc_sse2.hpp), dequant + mismatch control
+ *       (parse_block, mb_decoder.cpp:74-155), SSE2 IDCT put/add (idct_sse2.hpp:96-120) and
+ *       block placement (mb_decoder.cpp:166-196) — for a whole batch of pictures per call.
+ *       The seam is the packed record stream defined below (SURVEY.md §8b "Record stream").
+ *   mp2vg_parse_es
+ *       the host record emitter: start-code scan + header parse + VLC/MV/DC parse
+ *       (decoder.cpp:278-329, mp2v_hdr.cpp, mp2v_vlc_dec.hpp, mb_decoder.cpp:341-641) producing
+ *       records instead of pixels.
+ *   mp2vg_decoder_*
+ *       the drop-in decoder: mp2v_decoder_c(config, renderer) + decode(buf, len) with frames
+ *       delivered in display order on a render thread (decoder.h:82-131, decoder.cpp:346-379).
+ *       include/mp2v_decoder.h wraps these in the reference's own C++ class names.
+ */
+#ifndef MP2VG_H
+#define MP2VG_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MP2VG_ABI_VERSION 1
+
+/* ---- status codes --------------------------------------------------------------------- */
+enum {
+    MP2VG_OK = 0,
+    MP2VG_E_INVALID = -1,     /* bad argument / malformed record batch                    */
+    MP2VG_E_UNSUPPORTED = -2, /* stream outside the reference's decodable subset */
+    MP2VG_E_HIP = -3,         /* HIP runtime error (no device, launch failure, ...)        */
+    MP2VG_E_NOMEM = -4,
+    MP2VG_E_STATE = -5,       /* call out of order                                           */
+    MP2VG_E_BITSTREAM = -6    /* bitstream syntax error                                      */
+};
+
+/* ---- record stream (the seam; 32-byte MB records + 4-byte coefficient words) -------------
+ *
+ * One record per macroblock of every picture, skipped MBs included (as MC-only records), in
+ * raster order: picture p owns records [mb_first, mb_first + mb_width*mb_height).
+ * Motion vectors are FINAL luma vectors after all PMV rules and skipped-MB quirks
+ * (reference mb_decoder.cpp:447-519, 541-550, 580-604); chroma scaling stays on the device
+ * (mb_decoder.cpp:198-206).
+ */
+enum {
+    MP2VG_MB_INTRA = 1u << 0,     /* IDCT put, no MC                                         */
+    MP2VG_MB_FWD = 1u << 1,       /* forward prediction from fwd_slot                        */
+    MP2VG_MB_BWD = 1u << 2,       /* backward prediction from bwd_slot (both bits: bidir avg) */
+    MP2VG_MB_FIELD_MC = 1u << 3,  /* frame picture, field prediction: 2 vectors, 16x8 each  */
+    MP2VG_MB_DCT_FIELD = 1u << 4  /* dct_type = 1 (field DCT block placement)               */
+};
+/* motion_vertical_field_select[r][s] lives in flags bit (8 + 2*r + s) */
+#define MP2VG_MB_FS_BIT(r, s) (1u << (8 + 2 * (r) + (s)))
+
+typedef struct mp2vg_mb {
+    uint16_t x, y;        /* macroblock column / row                                          */
+    uint16_t flags;       /* MP2VG_MB_* | field selects                                        */
+    uint16_t cbp;         /* coded block pattern, bit b <-> block b (mb_decoder.cpp:421-445)   */
+    uint8_t  qscale;      /* quantiser_scale after q_scale_type mapping (decoder.cpp:140-145)  */
+    uint8_t  reserved;
+    uint16_t ncoef;       /* number of coefficient words                                        */
+    uint32_t coef_off;    /* index of the first coefficient word in the batch's coef array     */
+    int16_t  mv[2][2][2]; /* [vector r][direction s: 0 fwd, 1 bwd][x, y], half-pel luma units;
+                             field-MC vertical components in field units                       */
+} mp2vg_mb_t;             /* 32 bytes */
+
+/* Coefficient word: bits 0-15 int16 level (signed run-level level, or the final QFS[0] value
+ * when MP2VG_COEF_DC), bits 16-21 scan position i (0..63), bits 22-25 block index (0..11),
+ * bit 26 FIRST1S: non-intra first coefficient coded with the B.14 '1s' code — dequantised as
+ * (3*W[0]*qs)>>5 without the +-2047 clamp (mb_decoder.cpp:79-88), bit 27 DC: intra DC value,
+ * excluded from the mismatch parity (mb_decoder.cpp:76,160).  Words of one MB are grouped by
+ * block, blocks in bitstream order.                                                          */
+#define MP2VG_COEF_LEVEL(w) ((int16_t)((w) & 0xffffu))
+#define MP2VG_COEF_POS(w) (((w) >> 16) & 63u)
+#define MP2VG_COEF_BLOCK(w) (((w) >> 22) & 15u)
+#define MP2VG_COEF_FIRST1S (1u << 26)
+#define MP2VG_COEF_DC (1u << 27)
+#define MP2VG_COEF_PACK(level, pos, block, fl) \
+    ((uint32_t)(uint16_t)(int16_t)(level) | ((uint32_t)(pos) << 16) | ((uint32_t)(block) << 22) | (uint32_t)(fl))
+
+typedef struct mp2vg_picture {
+    int32_t  dst_slot;            /* frame-pool slot written                                   */
+    int32_t  fwd_slot;            /* forward reference slot (L0), -1 = none                    */
+    int32_t  bwd_slot;            /* backward reference slot (L1), -1 = none                   */
+    int32_t  picture_coding_type; /* 1 I, 2 P, 3 B                                              */
+    uint32_t mb_first;            /* first MB record of this picture                            */
+    uint16_t mb_width, mb_height;
+    uint8_t  alternate_scan;
+    uint8_t  reserved0[3];
+    int32_t  temporal_reference;
+    uint8_t  W[4][64];            /* quantiser matrices in scan order: [0] intra, [1] non-intra,
+                                     [2] chroma intra, [3] chroma non-intra (decoder.cpp:154-192) */
+} mp2vg_picture_t;                /* 288 bytes */
+
+/* ---- device context ------------------------------------------------------------------- */
+typedef struct mp2vg_config {
+    int32_t width, height;       /* CODED size (multiples of 16), as the reference's config  */
+    int32_t chroma_format;       /* 1 = 4:2:0, 2 = 4:2:2, 3 = 4:4:4                          */
+    int32_t pictures_pool_size;  /* number of device frame slots                             */
+    int32_t num_threads;         /* host parse threads (0 = auto)                            */
+    int32_t reordering;          /* display reorder in the drop-in decoder                   */
+    int32_t device;              /* HIP device ordinal                                       */
+    int32_t reserved;
+} mp2vg_config_t;
+
+typedef struct mp2vg_ctx mp2vg_ctx_t;
+
+int  mp2vg_abi_version(void);
+const char* mp2vg_status_string(int status);
+const char* mp2vg_last_error(void); /* thread-local detail of the last failure */
+
+int  mp2vg_create(const mp2vg_config_t* cfg, mp2vg_ctx_t** out);
+int  mp2vg_destroy(mp2vg_ctx_t* ctx);
+/* plane geometry of every frame slot: width/height/stride of plane 0..2, bytes per slot */
+int  mp2vg_frame_geometry(const mp2vg_config_t* cfg, int32_t width[3], int32_t height[3],
+                          int32_t stride[3], uint64_t* slot_bytes);
+/* resize the frame pool (slots are uninitialised) */
+int  mp2vg_reserve_slots(mp2vg_ctx_t* ctx, int32_t nslots);
+
+/* Upload a record batch from host memory (staged through pinned buffers, hipMemcpyAsync on the
+ * context stream).  The batch stays resident in HBM until the next upload. */
+int  mp2vg_batch_upload(mp2vg_ctx_t* ctx, const mp2vg_picture_t* pics, int32_t npics,
+                        const mp2vg_mb_t* mbs, uint64_t nmbs, const uint32_t* coefs,
+                        uint64_t ncoefs);
+/* Enqueue the reconstruct of every picture of the resident batch: pictures are grouped by
+ * reference-dependency depth and each depth level is one kernel launch (one workgroup per
+ * slice = MB row).  Asynchronous; per-launch device times are recorded with HIP events. */
+int  mp2vg_batch_decode(mp2vg_ctx_t* ctx);
+int  mp2vg_synchronize(mp2vg_ctx_t* ctx);
+/* number of kernel launches of the last mp2vg_batch_decode and their device times (ms) */
+int  mp2vg_last_launch_times(mp2vg_ctx_t* ctx, float* ms, int32_t max, int32_t* count);
+/* copy one frame slot to host planes (each plane written width x height, tightly packed if
+ * dst_stride is 0); synchronous */
+int  mp2vg_download_slot(mp2vg_ctx_t* ctx, int32_t slot, uint8_t* dst_planes[3],
+                         const int32_t dst_stride[3]);
+/* raw device pointer of a slot (for in-HBM consumers such as a digest kernel or RCCL) */
+int  mp2vg_slot_device_ptr(mp2vg_ctx_t* ctx, int32_t slot, void** dptr);
+/* 64-bit FNV-1a digest of each listed slot's visible planes, computed on device */
+int  mp2vg_slot_digests(mp2vg_ctx_t* ctx, const int32_t* slots, int32_t n, uint64_t* out);
+
+/* ---- host record emitter -------------------------------------------------------------- */
+typedef struct mp2vg_parsed mp2vg_parsed_t;
+
+/* Parse a whole elementary stream into records.  Pictures are numbered in decode order and
+ * slot ids are decode indices (dst_slot = i; refs point at earlier indices).  Validates the
+ * reference's input contract and returns MP2VG_E_UNSUPPORTED outside it. */
+int  mp2vg_parse_es(const uint8_t* buf, uint64_t len, const mp2vg_config_t* cfg,
+                    mp2vg_parsed_t** out);
+int  mp2vg_parsed_counts(const mp2vg_parsed_t* p, int32_t* npics, uint64_t* nmbs,
+                         uint64_t* ncoefs);
+const mp2vg_picture_t* mp2vg_parsed_pictures(const mp2vg_parsed_t* p);
+const mp2vg_mb_t*      mp2vg_parsed_mbs(const mp2vg_parsed_t* p);
+const uint32_t*        mp2vg_parsed_coefs(const mp2vg_parsed_t* p);
+/* display order (decode indices), as the reference's output scheduler emits them */
+int  mp2vg_parsed_display_order(const mp2vg_parsed_t* p, int32_t* order, int32_t n);
+/* GOP index (0-based, by group_start_code) of each picture, for GOP sharding */
+int  mp2vg_parsed_gop_index(const mp2vg_parsed_t* p, int32_t* gop, int32_t n);
+void mp2vg_parsed_free(mp2vg_parsed_t* p);
+
+/* ---- synthetic stream writer (the accepted subset only) --------------------- */
+typedef struct mp2vg_gen_params {
+    int32_t width, height, chroma_format;
+    int32_t n_gops;              /* closed GOPs                                              */
+    int32_t gop_n, gop_m;        /* N (pictures per GOP), M (anchor distance); M=1 -> no B  */
+    uint32_t seed;
+    int32_t frame_pred_frame_dct;/* 1: frame MC/DCT only; 0: field MC + field DCT allowed   */
+    int32_t alternate_scan;      /* 0, 1, or -1 = random per picture                        */
+    int32_t q_scale_type;        /* 0, 1, or -1 = random per picture                        */
+    int32_t intra_dc_precision;  /* 0..3, or -1 = random per picture                        */
+    int32_t coefs_min, coefs_max;/* AC coefficients per coded block                         */
+    int32_t intra_coefs_min, intra_coefs_max;
+    int32_t big_level_permille;  /* probability (per 1000) of a large escape level          */
+    int32_t escape_permille;     /* probability of forcing an escape code                   */
+    int32_t quant_permille;      /* probability an MB carries a new quantiser_scale         */
+    int32_t f_code;              /* motion f_code (1..9)                                     */
+    int32_t mix;                 /* 0: SURVEY §8d C2 mix; 1: intra only; 2: MC-heavy         */
+    int32_t leading_b;           /* closed GOP starts I + (M-1) backward-only B pictures    */
+    int32_t big_matrix_permille; /* probability of a quantiser-matrix entry > 128           */
+    int32_t reserved[5];
+} mp2vg_gen_params_t;
+
+void mp2vg_gen_default_params(mp2vg_gen_params_t* p);
+int  mp2vg_generate_es(const mp2vg_gen_params_t* p, uint8_t** out, uint64_t* len);
+void mp2vg_free(void* ptr);
+
+/* ---- drop-in decoder (reference mp2v_decoder_c) ---------------------------------------- */
+typedef struct mp2vg_frame {
+    uint8_t* planes[3];       /* host copy, valid only during the callback (frame_c rule)   */
+    int32_t  width[3], height[3], stride[3];
+    int32_t  picture_coding_type;
+    int32_t  decode_index;
+} mp2vg_frame_t;
+typedef void (*mp2vg_render_fn)(void* user, const mp2vg_frame_t* frame);
+typedef struct mp2vg_decoder mp2vg_decoder_t;
+
+int  mp2vg_decoder_create(const mp2vg_config_t* cfg, mp2vg_render_fn fn, void* user,
+                          mp2vg_decoder_t** out);
+/* decode a whole elementary stream (reference decode(): single-shot, synchronous; frames are
+ * delivered in display order to fn on a dedicated render thread before this returns) */
+int  mp2vg_decoder_decode(mp2vg_decoder_t* dec, const uint8_t* buf, uint64_t len);
+int  mp2vg_decoder_destroy(mp2vg_decoder_t* dec);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MP2VG_H */

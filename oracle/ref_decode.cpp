@@ -1,0 +1,81 @@
+// Test-infrastructure driver (ours) for the REAL reference decoder.
+//
+// Links the reference library built from /root/reference/src/core (see oracle/Makefile) and
+// drives it through its public API exactly like the reference CLI sample does
+// (reference tiny_decoder/tiny_mp2v_dec.cpp:11-17 write_yuv, :19-34 load_bitstream with 16 B
+// padding, :48 decoder construction, :50-55 timing around decode()), but with the
+// decoder_config_t taken from the command line instead of the sample's hard-coded
+// {1920,1088,2,10,8,true} (reference decoder.h:25-32).
+//
+// usage: ref_decode <in.m2v> <width> <height> <chroma_format 1|2|3> <threads> <out.yuv|-> [repeat]
+//   out "-" : decode without writing (timing mode).
+// prints one JSON line: {"frames": F, "ms": best-of-repeat decode() wall time, "threads": T}
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+#include "core/decoder.h"
+
+static void write_yuv(FILE* fp, frame_c* frame) {
+    for (int i = 0; i < 3; i++) {
+        uint8_t* plane = frame->get_planes(i);
+        for (int y = 0; y < frame->get_height(i); y++, plane += frame->get_strides(i))
+            fwrite(plane, 1, frame->get_width(i), fp);
+    }
+}
+
+int main(int argc, char** argv) {
+    if (argc < 7) {
+        fprintf(stderr, "usage: %s in.m2v width height chroma_format threads out.yuv|- [repeat]\n", argv[0]);
+        return 2;
+    }
+    FILE* in = fopen(argv[1], "rb");
+    if (!in) { perror(argv[1]); return 1; }
+    fseek(in, 0, SEEK_END);
+    long size = ftell(in);
+    fseek(in, 0, SEEK_SET);
+    long padded = (size + 15) & ~15L;
+    // The reference's SSE2 start-code scanner and bit reader read past the end of the buffer
+    // (start_codes_search.hpp:11-16, bitstream.h:20); keep 64 zero bytes of slack after it.
+    std::vector<uint8_t> buf(padded + 64, 0);
+    if (fread(buf.data(), 1, size, in) != (size_t)size) { perror("read"); return 1; }
+    fclose(in);
+
+    decoder_config_t cfg;
+    cfg.width = atoi(argv[2]);
+    cfg.height = atoi(argv[3]);
+    cfg.chroma_format = atoi(argv[4]);
+    cfg.pictures_pool_size = 10;
+    cfg.num_threads = atoi(argv[5]);
+    cfg.reordering = true;
+    const char* out_path = argv[6];
+    int repeat = argc > 7 ? atoi(argv[7]) : 1;
+
+    FILE* out = nullptr;
+    if (strcmp(out_path, "-") != 0) {
+        out = fopen(out_path, "wb");
+        if (!out) { perror(out_path); return 1; }
+    }
+    double best_ms = 1e30;
+    int frames = 0;
+    for (int r = 0; r < repeat; r++) {
+        int nframes = 0;
+        FILE* fp = (r == 0) ? out : nullptr;
+        auto t0 = std::chrono::steady_clock::now();
+        {
+            mp2v_decoder_c dec(cfg, [fp, &nframes](frame_c* f) {
+                nframes++;
+                if (fp) write_yuv(fp, f);
+            });
+            dec.decode(buf.data(), (int)padded);
+        }  // destructor joins the render + worker threads: all frames delivered
+        auto t1 = std::chrono::steady_clock::now();
+        double ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
+        if (ms < best_ms) best_ms = ms;
+        frames = nframes;
+    }
+    if (out) fclose(out);
+    printf("{\"frames\": %d, \"ms\": %.3f, \"threads\": %d}\n", frames, best_ms, cfg.num_threads);
+    return 0;
+}

@@ -1,0 +1,203 @@
+// decoder.cpp — drop-in decoder over the record path: the reference's mp2v_decoder_c behaviour
+// (decoder.h:82-131) on the GPU.
+//
+//   decode(buf, len)  (reference decoder.cpp:278-329): parse the whole elementary stream into
+//                     records on the host (multi-threaded, parse.cpp), then stream the pictures
+//                     through the device in decode-order chunks: each chunk is one record batch
+//                     (one launch per dependency level), frames are copied back into host frames
+//                     with the reference frame_c layout (stride = round_up(width, 64), planes
+//                     Y,U,V; decoder.cpp:44-77) and handed to the renderer.
+//   renderer          called on a dedicated render thread, in the reference's display order
+//                     (decoder.cpp:346-379: B pictures at once, I/P delayed by one anchor), with
+//                     a frame valid only for the duration of the call.
+//   decode() returns after every frame has been rendered (reference flush/kill semantics,
+//   decoder.cpp:244-254 + threads.cpp:198-211).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <condition_variable>
+#include <deque>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "syntax.h"
+
+using namespace mp2vg;
+
+namespace {
+constexpr int kChunk = 16;  // pictures per device batch
+
+struct HostFrame {
+    std::vector<uint8_t> data;
+    mp2vg_frame_t f;
+};
+}  // namespace
+
+struct mp2vg_decoder {
+    mp2vg_config_t cfg{};
+    mp2vg_render_fn fn = nullptr;
+    void* user = nullptr;
+    mp2vg_ctx_t* ctx = nullptr;
+    Geom g{};
+    int nslots = 0;
+};
+
+extern "C" int mp2vg_decoder_create(const mp2vg_config_t* cfg, mp2vg_render_fn fn, void* user,
+                                    mp2vg_decoder_t** out) {
+    if (!cfg || !fn || !out) return MP2VG_E_INVALID;
+    *out = nullptr;
+    mp2vg_config_t c = *cfg;
+    c.pictures_pool_size = std::max(cfg->pictures_pool_size, kChunk + 4);
+    mp2vg_ctx_t* ctx = nullptr;
+    int rc = mp2vg_create(&c, &ctx);
+    if (rc != MP2VG_OK) return rc;
+    auto* d = new mp2vg_decoder();
+    d->cfg = c;
+    d->fn = fn;
+    d->user = user;
+    d->ctx = ctx;
+    d->g.init(c.width, c.height, c.chroma_format);
+    d->nslots = c.pictures_pool_size;
+    *out = d;
+    return MP2VG_OK;
+}
+
+extern "C" int mp2vg_decoder_destroy(mp2vg_decoder_t* d) {
+    if (!d) return MP2VG_E_INVALID;
+    mp2vg_destroy(d->ctx);
+    delete d;
+    return MP2VG_OK;
+}
+
+extern "C" int mp2vg_decoder_decode(mp2vg_decoder_t* d, const uint8_t* buf, uint64_t len) {
+    if (!d || !buf) return MP2VG_E_INVALID;
+    mp2vg_parsed_t* parsed = nullptr;
+    int rc = mp2vg_parse_es(buf, len, &d->cfg, &parsed);
+    if (rc != MP2VG_OK) return rc;
+    std::unique_ptr<mp2vg_parsed_t, void (*)(mp2vg_parsed_t*)> guard(parsed, mp2vg_parsed_free);
+    int32_t npics = 0;
+    uint64_t nmbs = 0, ncoefs = 0;
+    mp2vg_parsed_counts(parsed, &npics, &nmbs, &ncoefs);
+    const mp2vg_picture_t* pics = mp2vg_parsed_pictures(parsed);
+    const mp2vg_mb_t* mbs = mp2vg_parsed_mbs(parsed);
+    const uint32_t* coefs = mp2vg_parsed_coefs(parsed);
+    std::vector<int32_t> display(npics);
+    if (npics) mp2vg_parsed_display_order(parsed, display.data(), npics);
+
+    // last decode index that predicts from each picture
+    std::vector<int> last_use(npics, -1);
+    for (int q = 0; q < npics; q++) {
+        if (pics[q].fwd_slot >= 0) last_use[pics[q].fwd_slot] = q;
+        if (pics[q].bwd_slot >= 0) last_use[pics[q].bwd_slot] = q;
+    }
+
+    // render thread (decoder.cpp:403, :346-379)
+    std::mutex mu;
+    std::condition_variable cv;
+    std::deque<std::unique_ptr<HostFrame>> q;
+    bool done = false;
+    std::thread render([&]() {
+        for (;;) {
+            std::unique_ptr<HostFrame> f;
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return done || !q.empty(); });
+                if (q.empty()) return;
+                f = std::move(q.front());
+                q.pop_front();
+            }
+            d->fn(d->user, &f->f);
+        }
+    });
+
+    std::vector<int> slot_of(npics, -1);
+    std::vector<int> free_slots;
+    for (int s = d->nslots - 1; s >= 0; s--) free_slots.push_back(s);
+    std::map<int, std::unique_ptr<HostFrame>> ready;  // decode index -> downloaded frame
+    size_t next_display = 0;
+    std::vector<mp2vg_picture_t> cp;
+    std::vector<mp2vg_mb_t> cm;
+    const uint64_t mbs_per_pic = (uint64_t)(d->cfg.width / 16) * (d->cfg.height / 16);
+
+    auto finish = [&](int status) {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            done = true;
+        }
+        cv.notify_all();
+        render.join();
+        return status;
+    };
+
+    for (int s = 0; s < npics; s += kChunk) {
+        int e = std::min(npics, s + kChunk);
+        // slots for this chunk
+        for (int p = s; p < e; p++) {
+            if (free_slots.empty()) return finish(MP2VG_E_STATE);
+            slot_of[p] = free_slots.back();
+            free_slots.pop_back();
+        }
+        // chunk records with physical slots; MB / coefficient ranges rebased
+        uint64_t mb0 = pics[s].mb_first, mb1 = pics[e - 1].mb_first + mbs_per_pic;
+        uint64_t c0 = ncoefs, c1 = 0;
+        for (uint64_t k = mb0; k < mb1; k++) {
+            c0 = std::min<uint64_t>(c0, mbs[k].coef_off);
+            c1 = std::max<uint64_t>(c1, (uint64_t)mbs[k].coef_off + mbs[k].ncoef);
+        }
+        if (c0 > c1) c0 = c1 = 0;
+        cp.assign(pics + s, pics + e);
+        for (auto& P : cp) {
+            P.dst_slot = slot_of[P.dst_slot];
+            if (P.fwd_slot >= 0) P.fwd_slot = slot_of[P.fwd_slot];
+            if (P.bwd_slot >= 0) P.bwd_slot = slot_of[P.bwd_slot];
+            P.mb_first -= (uint32_t)mb0;
+        }
+        cm.assign(mbs + mb0, mbs + mb1);
+        for (auto& m : cm) m.coef_off -= (uint32_t)c0;
+        rc = mp2vg_batch_upload(d->ctx, cp.data(), (int32_t)cp.size(), cm.data(), cm.size(), coefs + c0, c1 - c0);
+        if (rc == MP2VG_OK) rc = mp2vg_batch_decode(d->ctx);
+        if (rc == MP2VG_OK) rc = mp2vg_synchronize(d->ctx);
+        if (rc != MP2VG_OK) return finish(rc);
+        // download into frame_c-layout host frames
+        for (int p = s; p < e; p++) {
+            auto hf = std::make_unique<HostFrame>();
+            hf->data.resize(d->g.slot_bytes);
+            uint8_t* planes[3];
+            int32_t strides[3];
+            for (int i = 0; i < 3; i++) {
+                planes[i] = hf->data.data() + d->g.plane_off[i];
+                strides[i] = d->g.stride[i];
+                hf->f.planes[i] = planes[i];
+                hf->f.width[i] = d->g.pw[i];
+                hf->f.height[i] = d->g.ph[i];
+                hf->f.stride[i] = d->g.stride[i];
+            }
+            hf->f.picture_coding_type = pics[p].picture_coding_type;
+            hf->f.decode_index = p;
+            rc = mp2vg_download_slot(d->ctx, slot_of[p], planes, strides);
+            if (rc != MP2VG_OK) return finish(rc);
+            ready[p] = std::move(hf);
+        }
+        // release slots no later picture predicts from
+        for (int p = 0; p < e; p++)
+            if (slot_of[p] >= 0 && last_use[p] < e) {
+                free_slots.push_back(slot_of[p]);
+                slot_of[p] = -1;
+            }
+        // hand frames to the render thread in display order
+        while (next_display < display.size() && ready.count(display[next_display])) {
+            auto it = ready.find(display[next_display]);
+            {
+                std::lock_guard<std::mutex> lk(mu);
+                q.push_back(std::move(it->second));
+            }
+            cv.notify_one();
+            ready.erase(it);
+            next_display++;
+        }
+    }
+    return finish(next_display == display.size() ? MP2VG_OK : MP2VG_E_STATE);
+}

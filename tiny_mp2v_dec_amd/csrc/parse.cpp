@@ -1,0 +1,642 @@
+// parse.cpp — host record emitter: MPEG-2 elementary stream -> record stream (include/mp2vg.h).
+//
+// Reproduces the REFERENCE's parse semantics, quirks included, so that the
+// records drive the device reconstruct to the reference's exact output:
+//   start-code dispatch              decoder.cpp:278-329
+//   header parsers                   mp2v_hdr.cpp:4-223, slice header mp2v_hdr.h:345-363
+//   W matrices from the QME only     decoder.cpp:154-192
+//   slice setup                      decoder.cpp:107-145
+//   macroblock parse                 mb_decoder.cpp:341-641 (parse_modes, cbp, MVs, PMV rules,
+//                                    skipped MBs, DC prediction, parse_block's VLC loop)
+// Where the reference has undefined behaviour the stream is rejected (MP2VG_E_UNSUPPORTED):
+// missing QME / partial loads, intra MBs with intra_vlc_format=0, field pictures, dual-prime,
+// slices not starting at column 0, skipped MBs in I pictures, MC reads outside the reference
+// planes, 4:4:4 with field DCT (reference writes blocks 10/11 outside the MB), concealment MVs in
+// P/B pictures, scalable extensions.
+#include <algorithm>
+#include <atomic>
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "syntax.h"
+
+namespace mp2vg {
+
+namespace {
+
+struct PictureHdr {
+    int pct = 0;
+    int temporal_reference = 0;
+    int f_code[2][2] = {{15, 15}, {15, 15}};
+    int intra_dc_precision = 0;
+    int picture_structure = 3;
+    int frame_pred_frame_dct = 1;
+    int concealment_motion_vectors = 0;
+    int q_scale_type = 0;
+    int intra_vlc_format = 0;
+    int alternate_scan = 0;
+    bool have_pcext = false;
+    bool have_qme = false;
+    int qme_load[4] = {0, 0, 0, 0};
+    uint8_t qme[4][64] = {};
+};
+
+struct SliceJob {
+    int pic;                  // decode index
+    uint64_t byte_off;        // offset of the slice start code
+    uint64_t byte_end;        // end of the slice payload (next start code)
+};
+
+struct PicWork {
+    PictureHdr hdr;
+    int fwd = -1, bwd = -1;   // decode indices of reference pictures (L0 / L1)
+    int gop = -1;
+    uint8_t W[4][64] = {};
+    std::vector<SliceJob> slices;
+};
+
+struct SliceOut {
+    std::vector<uint32_t> coefs;
+    int mb_row = -1;
+    int status = MP2VG_OK;
+    std::string err;
+};
+
+struct Ctx {
+    const uint8_t* buf;
+    uint64_t len;
+    Geom g;
+    int width, height, mbw, mbh;
+    int vertical_size_value = 0;
+    std::vector<PicWork> pics;
+};
+
+#define FAIL(code, msg)          \
+    do {                         \
+        out.status = (code);     \
+        out.err = (msg);         \
+        return;                  \
+    } while (0)
+
+// One slice -> its MB row of records (mb_decoder.cpp:521-641 for every MB of the slice).
+void parse_slice(const Ctx& C, const PicWork& P, const SliceJob& job, mp2vg_mb_t* row_base_all,
+                 std::vector<uint8_t>& row_done, SliceOut& out) {
+    const Tables& T = Tables::get();
+    const PictureHdr& h = P.hdr;
+    const int pct = h.pct;
+    const int cf = C.g.cf;
+    const int nblocks = C.g.nblocks;
+    BitReader br(C.buf + job.byte_off, C.buf + job.byte_end);
+
+    // slice header (mp2v_hdr.h:345-363)
+    br.skip(24);
+    int vpos = (int)br.read(8);
+    int mb_row;
+    if (C.vertical_size_value > 2800) {
+        int ext = (int)br.read(3);
+        mb_row = (ext << 7) + vpos - 1;
+    } else {
+        mb_row = vpos - 1;
+    }
+    int qcode = (int)br.read(5);
+    if (br.peek(1) == 1) {
+        br.skip(1 + 1 + 1 + 6);
+        while (br.peek(1) == 1) br.skip(9);
+    }
+    br.skip(1);
+    if (mb_row < 0 || mb_row >= C.mbh) FAIL(MP2VG_E_UNSUPPORTED, "slice row outside the picture");
+    if (row_done[mb_row]) FAIL(MP2VG_E_UNSUPPORTED, "two slices in one macroblock row");
+    row_done[mb_row] = 1;
+    out.mb_row = mb_row;
+
+    // cache setup (decoder.cpp:125-145)
+    int16_t PMVs[2][2][2] = {};
+    uint16_t dc_pred[3];
+    const uint16_t dc_reset = (uint16_t)(1 << (h.intra_dc_precision + 7));
+    dc_pred[0] = dc_pred[1] = dc_pred[2] = dc_reset;
+    int qscale = qscale_from_code(qcode, h.q_scale_type);
+    uint32_t previous_mb_type = 0;
+    mp2vg_mb_t* row = row_base_all + (size_t)mb_row * C.mbw;
+    int x = 0;
+    const int pstruct_frame = 1;  // only frame pictures are accepted
+    (void)pstruct_frame;
+
+    auto emit_skipped = [&](int xx) -> bool {
+        mp2vg_mb_t& m = row[xx];
+        memset(&m, 0, sizeof(m));
+        m.x = (uint16_t)xx;
+        m.y = (uint16_t)mb_row;
+        m.qscale = (uint8_t)qscale;
+        m.coef_off = (uint32_t)out.coefs.size();
+        // base_motion_compensation<cf, frame, two_vect = (B), skipped=true>(cache, mb, cache.PMVs)
+        // (mb_decoder.cpp:546-548, :291-339): direction from previous_mb_type; in B frame
+        // pictures vector 1 overwrites vector 0, so the effective vectors are PMVs[1][*].
+        uint32_t t = previous_mb_type;
+        bool fwd = t & MBT_FWD, bwd = t & MBT_BWD;
+        if (!fwd && !bwd) fwd = true;  // 'else' branch: forward
+        m.flags = (uint16_t)((fwd ? MP2VG_MB_FWD : 0) | (bwd ? MP2VG_MB_BWD : 0));
+        int vsel = (pct == 3) ? 1 : 0;
+        for (int s = 0; s < 2; s++)
+            for (int c = 0; c < 2; c++) m.mv[0][s][c] = PMVs[vsel][s][c];
+        for (int s = 0; s < 2; s++) {
+            if (!((s == 0 && fwd) || (s == 1 && bwd))) continue;
+            if ((s == 0 ? P.fwd : P.bwd) < 0) return false;
+            if (!mc_reads_inside(C.g, xx, mb_row, m.mv[0][s][0], m.mv[0][s][1], false, 0, 0))
+                return false;
+        }
+        return true;
+    };
+
+    do {
+        if (x >= C.mbw) FAIL(MP2VG_E_BITSTREAM, "macroblock beyond the end of the row");
+        // macroblock_address_increment (mb_decoder.cpp:534-539)
+        int inc = 0;
+        while (br.peek(11) == 0x008) {
+            br.skip(11);
+            inc += 33;
+        }
+        int e = T.mba.decode(br);
+        if (e < 0 || e >= 33) FAIL(MP2VG_E_BITSTREAM, "bad macroblock_address_increment");
+        inc += kMbaCodes[e].a;
+        if (x == 0 && inc != 1) FAIL(MP2VG_E_UNSUPPORTED, "slice does not start at column 0");
+        // skipped macroblocks (mb_decoder.cpp:541-550)
+        if (inc > 1) {
+            if (pct == 1) FAIL(MP2VG_E_UNSUPPORTED, "skipped macroblock in an I picture");
+            if (pct == 2) memset(PMVs, 0, sizeof(PMVs));
+            for (int i = 0; i < inc - 1; i++) {
+                if (x >= C.mbw) FAIL(MP2VG_E_BITSTREAM, "skip run beyond the end of the row");
+                if (!emit_skipped(x)) FAIL(MP2VG_E_UNSUPPORTED, "skipped MB reads outside the reference");
+                x++;
+            }
+        }
+        if (x >= C.mbw) FAIL(MP2VG_E_BITSTREAM, "macroblock beyond the end of the row");
+
+        // macroblock_modes (parse_modes, mb_decoder.cpp:341-419)
+        int te = T.mbtype[pct].decode(br);
+        if (te < 0) FAIL(MP2VG_E_BITSTREAM, "bad macroblock_type");
+        uint32_t mbt = (pct == 1 ? kMbTypeI : pct == 2 ? kMbTypeP : kMbTypeB)[te].a;
+        const bool intra = mbt & MBT_INTRA;
+        const bool mfwd = mbt & MBT_FWD, mbwd = mbt & MBT_BWD, pattern = mbt & MBT_PATTERN;
+        int frame_motion_type = 2;
+        if ((mfwd || mbwd) && h.frame_pred_frame_dct == 0) frame_motion_type = (int)br.read(2);
+        int dct_type = 0;
+        if (h.frame_pred_frame_dct == 0 && (intra || pattern)) dct_type = (int)br.read(1);
+        bool field_mv = false;  // mv_format == Field
+        int mv_count = 1;
+        if (!intra && (mfwd || mbwd)) {
+            if (frame_motion_type == 1) {
+                field_mv = true;
+                mv_count = 2;
+            } else if (frame_motion_type == 3) {
+                FAIL(MP2VG_E_UNSUPPORTED, "dual-prime prediction");
+            } else if (frame_motion_type != 2) {
+                FAIL(MP2VG_E_BITSTREAM, "reserved frame_motion_type");
+            }
+        }
+        if (mbt & MBT_QUANT) qscale = qscale_from_code((int)br.read(5), h.q_scale_type);
+        if (cf == 3 && dct_type && (intra || pattern))
+            FAIL(MP2VG_E_UNSUPPORTED, "4:4:4 field DCT (reference misplaces blocks 10/11)");
+
+        // motion_vectors (mb_decoder.cpp:479-519, 565-574)
+        int16_t MVs[2][2][2] = {};
+        int fsel[2][2] = {};
+        auto parse_mv = [&](int r, int s) -> bool {
+            for (int t = 0; t < 2; t++) {
+                int ci = T.motion.decode(br);
+                if (ci < 0) return false;
+                int mc = kMotionCodes[ci].a;
+                if (mc && br.read(1)) mc = -mc;
+                int fc = h.f_code[s][t];
+                int residual = 0;
+                if (fc != 1 && mc != 0) residual = (int)br.read(fc - 1);
+                MVs[r][s][t] = mv_reconstruct(fc, mc, residual, PMVs[r][s][t], field_mv && t == 1);
+            }
+            return true;
+        };
+        auto parse_mvs = [&](int s) -> bool {
+            if (mv_count == 1) {
+                if (field_mv) fsel[0][s] = (int)br.read(1);
+                return parse_mv(0, s);
+            }
+            fsel[0][s] = (int)br.read(1);
+            if (!parse_mv(0, s)) return false;
+            fsel[1][s] = (int)br.read(1);
+            return parse_mv(1, s);
+        };
+        const bool cmv = h.concealment_motion_vectors && pct == 1;
+        if (mfwd || (intra && cmv))
+            if (!parse_mvs(0)) FAIL(MP2VG_E_BITSTREAM, "bad motion_code");
+        if (mbwd)
+            if (!parse_mvs(1)) FAIL(MP2VG_E_BITSTREAM, "bad motion_code");
+        if (intra && cmv) br.skip(1);
+
+        // PMV update + MC selection (mb_decoder.cpp:580-620)
+        mp2vg_mb_t& m = row[x];
+        memset(&m, 0, sizeof(m));
+        m.x = (uint16_t)x;
+        m.y = (uint16_t)mb_row;
+        if (pct != 1) {
+            bool frame_based = intra || !field_mv;  // prediction_type == Frame_based
+            if (frame_based) {
+                if (intra) {
+                    for (int t = 0; t < 2; t++) PMVs[1][0][t] = PMVs[0][0][t];
+                } else if (mfwd && mbwd) {
+                    for (int t = 0; t < 2; t++) {
+                        PMVs[1][0][t] = PMVs[0][0][t];
+                        PMVs[1][1][t] = PMVs[0][1][t];
+                    }
+                } else if (mfwd) {
+                    for (int t = 0; t < 2; t++) PMVs[1][0][t] = PMVs[0][0][t];
+                } else if (mbwd) {
+                    for (int t = 0; t < 2; t++) PMVs[1][1][t] = PMVs[0][1][t];
+                }
+            }
+            bool no_mc_p = (pct == 2 && !intra && !mfwd);
+            if (intra || no_mc_p) {  // concealment is never on in P/B templates
+                memset(PMVs, 0, sizeof(PMVs));
+                memset(MVs, 0, sizeof(MVs));
+                field_mv = false;
+            }
+            if (!intra) {
+                bool fwd = mfwd || no_mc_p, bwd = mbwd;
+                m.flags = (uint16_t)((fwd ? MP2VG_MB_FWD : 0) | (bwd ? MP2VG_MB_BWD : 0) |
+                                     (field_mv ? MP2VG_MB_FIELD_MC : 0));
+                int nv = field_mv ? 2 : 1;
+                for (int r = 0; r < nv; r++)
+                    for (int s = 0; s < 2; s++) {
+                        if (!((s == 0 && fwd) || (s == 1 && bwd))) continue;
+                        if ((s == 0 ? P.fwd : P.bwd) < 0)
+                            FAIL(MP2VG_E_UNSUPPORTED, "prediction from a missing reference");
+                        m.mv[r][s][0] = MVs[r][s][0];
+                        m.mv[r][s][1] = MVs[r][s][1];
+                        if (field_mv && fsel[r][s]) m.flags |= (uint16_t)MP2VG_MB_FS_BIT(r, s);
+                        if (!mc_reads_inside(C.g, x, mb_row, MVs[r][s][0], MVs[r][s][1], field_mv,
+                                             fsel[r][s], r))
+                            FAIL(MP2VG_E_UNSUPPORTED, "motion vector reads outside the reference");
+                    }
+            }
+        }
+        if (intra) m.flags |= MP2VG_MB_INTRA;
+
+        // dct_dc_pred reset (mb_decoder.cpp:623-626)
+        if (inc > 1 || !intra) dc_pred[0] = dc_pred[1] = dc_pred[2] = dc_reset;
+
+        // coded_block_pattern (mb_decoder.cpp:421-445, 628-631)
+        uint32_t cbp = intra ? 0xfffu : 0;
+        if (pattern) {
+            int ci = T.cbp.decode(br);
+            if (ci < 0) FAIL(MP2VG_E_BITSTREAM, "bad coded_block_pattern");
+            uint32_t v = (uint32_t)kCbpCodes[ci].a;
+            uint32_t c1 = 0, c2 = 0;
+            if (cf == 2) c1 = br.read(2);
+            if (cf == 3) c2 = br.read(6);
+            for (int i = 0; i < 6; i++)
+                if (v & (1u << (5 - i))) cbp |= 1u << i;
+            if (cf == 2)
+                for (int i = 6; i < 8; i++)
+                    if (c1 & (1u << (7 - i))) cbp |= 1u << i;
+            if (cf == 3)
+                for (int i = 6; i < 12; i++)
+                    if (c2 & (1u << (11 - i))) cbp |= 1u << i;
+        }
+        cbp &= (1u << nblocks) - 1;
+        if (dct_type && (intra || pattern)) m.flags |= MP2VG_MB_DCT_FIELD;
+        m.cbp = (uint16_t)cbp;
+        m.qscale = (uint8_t)qscale;
+        m.coef_off = (uint32_t)out.coefs.size();
+
+        // blocks (decode_transform_template / decode_block_template / parse_block)
+        if (intra && h.intra_vlc_format == 0)
+            FAIL(MP2VG_E_UNSUPPORTED, "intra macroblock with intra_vlc_format=0 (reference mis-parses)");
+        const int tab = intra ? 1 : 0;
+        const VlcLut& cl = T.coef[tab];
+        for (int b = 0; b < nblocks; b++) {
+            if (!(cbp & (1u << b))) continue;
+            int i = 0;
+            if (intra) {
+                // parse_dct_dc_coeff (mb_decoder.cpp:46-72)
+                int pidx = b < 4 ? 0 : ((b & 1) ? 2 : 1);
+                int si = (b < 4 ? T.dc_luma : T.dc_chroma).decode(br);
+                if (si < 0) FAIL(MP2VG_E_BITSTREAM, "bad dct_dc_size");
+                int size = (b < 4 ? kDcSizeLuma : kDcSizeChroma)[si].a;
+                int diff = 0;
+                if (size) {
+                    int d = (int)br.read(size);
+                    int half = 1 << (size - 1);
+                    diff = d >= half ? d : (d + 1) - 2 * half;
+                }
+                dc_pred[pidx] = (uint16_t)(dc_pred[pidx] + diff);
+                int16_t dcv = (int16_t)(dc_pred[pidx] << (3 - h.intra_dc_precision));
+                out.coefs.push_back(MP2VG_COEF_PACK(dcv, 0, b, MP2VG_COEF_DC));
+                i = 1;
+            } else {
+                // non-intra first coefficient '1s' (mb_decoder.cpp:79-88)
+                uint32_t c = br.peek(2);
+                if (c & 2) {
+                    int lvl = (c & 1) ? -1 : 1;
+                    out.coefs.push_back(MP2VG_COEF_PACK(lvl, 0, b, MP2VG_COEF_FIRST1S));
+                    br.skip(2);
+                    i = 1;
+                }
+            }
+            for (;;) {
+                int ci = cl.decode(br);
+                if (ci < 0) FAIL(MP2VG_E_BITSTREAM, "bad DCT coefficient code");
+                if (ci == Tables::COEF_EOB) break;
+                int run, level;
+                if (ci == Tables::COEF_ESC) {
+                    run = (int)br.read(6);
+                    int v = (int)br.read(12);
+                    level = (v & 0x800) ? v - 4096 : v;  // signed 12-bit (:100-104)
+                } else {
+                    run = T.coef_run[tab][ci];
+                    level = T.coef_level[tab][ci];
+                    if (br.read(1)) level = -level;
+                }
+                i += run;
+                if (i > 63) FAIL(MP2VG_E_BITSTREAM, "coefficient run past position 63");
+                out.coefs.push_back(MP2VG_COEF_PACK(level, i, b, 0));
+                i++;
+            }
+        }
+        size_t nc = out.coefs.size() - m.coef_off;
+        m.ncoef = (uint16_t)nc;
+        if (br.overrun()) FAIL(MP2VG_E_BITSTREAM, "slice overruns the buffer");
+        previous_mb_type = mbt;
+        x++;
+    } while (br.peek(23) != 0);
+    if (x != C.mbw) FAIL(MP2VG_E_UNSUPPORTED, "slice does not cover the whole macroblock row");
+}
+
+#undef FAIL
+
+}  // namespace
+
+struct ParsedImpl {
+    std::vector<mp2vg_picture_t> pics;
+    std::vector<mp2vg_mb_t> mbs;
+    std::vector<uint32_t> coefs;
+    std::vector<int32_t> display;
+    std::vector<int32_t> gop;
+};
+
+}  // namespace mp2vg
+
+struct mp2vg_parsed : mp2vg::ParsedImpl {};
+
+using namespace mp2vg;
+
+extern "C" int mp2vg_parse_es(const uint8_t* buf, uint64_t len, const mp2vg_config_t* cfg,
+                              mp2vg_parsed_t** out) {
+    if (!buf || !cfg || !out) return MP2VG_E_INVALID;
+    *out = nullptr;
+    if (mp2vg_frame_geometry(cfg, nullptr, nullptr, nullptr, nullptr) != MP2VG_OK) return MP2VG_E_INVALID;
+    Ctx C;
+    C.buf = buf;
+    C.len = len;
+    C.width = cfg->width;
+    C.height = cfg->height;
+    C.mbw = cfg->width / 16;
+    C.mbh = cfg->height / 16;
+    C.g.init(cfg->width, cfg->height, cfg->chroma_format);
+
+    // ---- pass 1: start codes and headers, serially (decoder.cpp:278-329) ----
+    std::vector<uint64_t> sc;
+    for (uint64_t i = 0; i + 3 < len; i++)
+        if (buf[i] == 0 && buf[i + 1] == 0 && buf[i + 2] == 1) {
+            sc.push_back(i);
+            i += 2;
+        }
+    int seq_chroma = -1;
+    int cur = -1;
+    int gop = -1;
+    int ref_frames[2] = {-1, -1};
+    bool seq_end = false;
+    for (size_t k = 0; k < sc.size() && !seq_end; k++) {
+        uint64_t off = sc[k];
+        uint64_t end = (k + 1 < sc.size()) ? sc[k + 1] : len;
+        uint8_t code = buf[off + 3];
+        BitReader br(buf + off, buf + end);
+        br.skip(32);
+        if (code == 0xB3) {  // sequence_header (mp2v_hdr.cpp:4-21)
+            br.skip(12);
+            C.vertical_size_value = (int)br.read(12);
+        } else if (code == 0xB5) {  // extension (decoder.cpp:202-242)
+            int id = (int)br.read(4);
+            if (id == 1) {  // sequence_extension (mp2v_hdr.cpp:23-37)
+                br.skip(8 + 1);
+                seq_chroma = (int)br.read(2);
+            } else if (id == 5) {
+                set_error("scalable extensions are not supported by the reference path");
+                return MP2VG_E_UNSUPPORTED;
+            } else if (id == 8 && cur >= 0) {  // picture_coding_extension (:105-131)
+                PictureHdr& h = C.pics[cur].hdr;
+                for (int s = 0; s < 2; s++)
+                    for (int t = 0; t < 2; t++) h.f_code[s][t] = (int)br.read(4);
+                h.intra_dc_precision = (int)br.read(2);
+                h.picture_structure = (int)br.read(2);
+                br.skip(1);  // top_field_first
+                h.frame_pred_frame_dct = (int)br.read(1);
+                h.concealment_motion_vectors = (int)br.read(1);
+                h.q_scale_type = (int)br.read(1);
+                h.intra_vlc_format = (int)br.read(1);
+                h.alternate_scan = (int)br.read(1);
+                h.have_pcext = true;
+            } else if (id == 3 && cur >= 0) {  // quant_matrix_extension (:133-152)
+                PictureHdr& h = C.pics[cur].hdr;
+                h.have_qme = true;
+                for (int m = 0; m < 4; m++) {
+                    h.qme_load[m] = (int)br.read(1);
+                    if (h.qme_load[m])
+                        for (int i = 0; i < 64; i++) h.qme[m][i] = (uint8_t)br.read(8);
+                }
+            }
+        } else if (code == 0xB8) {  // group_of_pictures_header
+            gop++;
+        } else if (code == 0x00) {  // picture_start_code (decoder.cpp:294-305)
+            PicWork pw;
+            pw.hdr.temporal_reference = (int)br.read(10);
+            pw.hdr.pct = (int)br.read(3);
+            pw.gop = gop < 0 ? 0 : gop;
+            if (pw.hdr.pct < 1 || pw.hdr.pct > 3) {
+                set_error("unsupported picture_coding_type");
+                return MP2VG_E_UNSUPPORTED;
+            }
+            int idx = (int)C.pics.size();
+            if (pw.hdr.pct != 3) {
+                pw.fwd = ref_frames[1];  // I/P: dependency on the newest anchor (L0)
+                ref_frames[0] = ref_frames[1];
+                ref_frames[1] = idx;
+            } else {
+                pw.fwd = ref_frames[0];
+                pw.bwd = ref_frames[1];
+            }
+            if (pw.hdr.pct == 1) pw.fwd = -1;  // I pictures never predict
+            C.pics.push_back(pw);
+            cur = idx;
+        } else if (code >= 0x01 && code <= 0xAF) {
+            if (cur < 0) {
+                set_error("slice before the first picture");
+                return MP2VG_E_BITSTREAM;
+            }
+            C.pics[cur].slices.push_back({cur, off, end});
+        } else if (code == 0xB7 || code == 0xB4) {
+            seq_end = true;
+        }
+    }
+    if (seq_chroma >= 0 && seq_chroma != cfg->chroma_format) {
+        set_error("stream chroma_format differs from the decoder configuration");
+        return MP2VG_E_UNSUPPORTED;
+    }
+    // ---- picture-level validation + W (decoder.cpp:154-192) ----
+    for (auto& P : C.pics) {
+        PictureHdr& h = P.hdr;
+        if (!h.have_pcext) { set_error("MPEG-1 picture (no picture_coding_extension)"); return MP2VG_E_UNSUPPORTED; }
+        if (h.picture_structure != 3) { set_error("field pictures"); return MP2VG_E_UNSUPPORTED; }
+        if (!h.have_qme || !(h.qme_load[0] && h.qme_load[1] && h.qme_load[2] && h.qme_load[3])) {
+            set_error("picture without a full quant_matrix_extension (reference decoder.cpp:185-191)");
+            return MP2VG_E_UNSUPPORTED;
+        }
+        if (h.concealment_motion_vectors && h.pct != 1) {
+            set_error("concealment motion vectors in a P/B picture");
+            return MP2VG_E_UNSUPPORTED;
+        }
+        if (h.pct == 2 && P.fwd < 0) { set_error("P picture without a reference"); return MP2VG_E_UNSUPPORTED; }
+        if (P.slices.empty()) { set_error("picture without slices"); return MP2VG_E_BITSTREAM; }
+        build_W(h.qme, h.alternate_scan, P.W);
+    }
+    // ---- pass 2: slices (independent given picture state) in parallel ----
+    const int npics = (int)C.pics.size();
+    const size_t mbs_per_pic = (size_t)C.mbw * C.mbh;
+    auto* res = new mp2vg_parsed();
+    res->mbs.resize(mbs_per_pic * npics);
+    std::vector<SliceJob> jobs;
+    for (auto& P : C.pics)
+        for (auto& j : P.slices) jobs.push_back(j);
+    std::vector<SliceOut> outs(jobs.size());
+    std::vector<std::vector<uint8_t>> row_done(npics, std::vector<uint8_t>(C.mbh, 0));
+    // rows of one picture are claimed by one thread at a time: partition jobs by picture
+    std::atomic<int> next_pic(0);
+    std::vector<size_t> pic_job_begin(npics + 1, 0);
+    {
+        size_t j = 0;
+        for (int p = 0; p < npics; p++) {
+            pic_job_begin[p] = j;
+            j += C.pics[p].slices.size();
+        }
+        pic_job_begin[npics] = j;
+    }
+    int nthreads = cfg->num_threads > 0 ? cfg->num_threads : (int)std::thread::hardware_concurrency();
+    nthreads = std::max(1, std::min(nthreads, std::max(1, npics)));
+    auto worker = [&]() {
+        for (;;) {
+            int p = next_pic.fetch_add(1);
+            if (p >= npics) return;
+            for (size_t j = pic_job_begin[p]; j < pic_job_begin[p + 1]; j++)
+                parse_slice(C, C.pics[p], jobs[j], res->mbs.data() + mbs_per_pic * p, row_done[p], outs[j]);
+        }
+    };
+    if (nthreads == 1) {
+        worker();
+    } else {
+        std::vector<std::thread> th;
+        for (int t = 0; t < nthreads; t++) th.emplace_back(worker);
+        for (auto& t : th) t.join();
+    }
+    for (size_t j = 0; j < jobs.size(); j++)
+        if (outs[j].status != MP2VG_OK) {
+            char msg[256];
+            snprintf(msg, sizeof msg, "picture %d slice @%llu: %s", jobs[j].pic,
+                     (unsigned long long)jobs[j].byte_off, outs[j].err.c_str());
+            set_error(msg);
+            int st = outs[j].status;
+            delete res;
+            return st;
+        }
+    for (int p = 0; p < npics; p++)
+        for (int r = 0; r < C.mbh; r++)
+            if (!row_done[p][r]) {
+                set_error("picture with a macroblock row not covered by any slice");
+                delete res;
+                return MP2VG_E_UNSUPPORTED;
+            }
+    // ---- concatenate coefficients, fix offsets ----
+    size_t total = 0;
+    for (auto& o : outs) total += o.coefs.size();
+    if (total >= (1ull << 32)) {
+        delete res;
+        set_error("batch too large");
+        return MP2VG_E_INVALID;
+    }
+    res->coefs.resize(total);
+    {
+        size_t base = 0;
+        for (size_t j = 0; j < jobs.size(); j++) {
+            const SliceOut& o = outs[j];
+            if (!o.coefs.empty()) memcpy(&res->coefs[base], o.coefs.data(), o.coefs.size() * 4);
+            int p = jobs[j].pic;
+            mp2vg_mb_t* row = res->mbs.data() + mbs_per_pic * p + (size_t)o.mb_row * C.mbw;
+            for (int x = 0; x < C.mbw; x++) row[x].coef_off += (uint32_t)base;
+            base += o.coefs.size();
+        }
+    }
+    // ---- picture records ----
+    res->pics.resize(npics);
+    for (int p = 0; p < npics; p++) {
+        mp2vg_picture_t& d = res->pics[p];
+        memset(&d, 0, sizeof d);
+        const PicWork& P = C.pics[p];
+        d.dst_slot = p;
+        d.fwd_slot = P.fwd;
+        d.bwd_slot = P.hdr.pct == 3 ? P.bwd : -1;
+        d.picture_coding_type = P.hdr.pct;
+        d.mb_first = (uint32_t)(mbs_per_pic * p);
+        d.mb_width = (uint16_t)C.mbw;
+        d.mb_height = (uint16_t)C.mbh;
+        d.alternate_scan = (uint8_t)P.hdr.alternate_scan;
+        d.temporal_reference = P.hdr.temporal_reference;
+        memcpy(d.W, P.W, sizeof d.W);
+        res->gop.push_back(P.gop);
+    }
+    // ---- display order: the reference's output scheduler (decoder.cpp:346-369) ----
+    {
+        int held = -1;
+        for (int p = 0; p < npics; p++) {
+            if (C.pics[p].hdr.pct == 3 || !cfg->reordering) {
+                res->display.push_back(p);
+            } else {
+                if (held >= 0) res->display.push_back(held);
+                held = p;
+            }
+        }
+        if (held >= 0) res->display.push_back(held);
+    }
+    *out = res;
+    return MP2VG_OK;
+}
+
+extern "C" int mp2vg_parsed_counts(const mp2vg_parsed_t* p, int32_t* npics, uint64_t* nmbs,
+                                   uint64_t* ncoefs) {
+    if (!p) return MP2VG_E_INVALID;
+    if (npics) *npics = (int32_t)p->pics.size();
+    if (nmbs) *nmbs = p->mbs.size();
+    if (ncoefs) *ncoefs = p->coefs.size();
+    return MP2VG_OK;
+}
+extern "C" const mp2vg_picture_t* mp2vg_parsed_pictures(const mp2vg_parsed_t* p) { return p ? p->pics.data() : nullptr; }
+extern "C" const mp2vg_mb_t* mp2vg_parsed_mbs(const mp2vg_parsed_t* p) { return p ? p->mbs.data() : nullptr; }
+extern "C" const uint32_t* mp2vg_parsed_coefs(const mp2vg_parsed_t* p) { return p ? p->coefs.data() : nullptr; }
+extern "C" int mp2vg_parsed_display_order(const mp2vg_parsed_t* p, int32_t* order, int32_t n) {
+    if (!p || !order || n < (int32_t)p->display.size()) return MP2VG_E_INVALID;
+    memcpy(order, p->display.data(), p->display.size() * 4);
+    return (int)p->display.size();
+}
+extern "C" int mp2vg_parsed_gop_index(const mp2vg_parsed_t* p, int32_t* gop, int32_t n) {
+    if (!p || !gop || n < (int32_t)p->gop.size()) return MP2VG_E_INVALID;
+    memcpy(gop, p->gop.data(), p->gop.size() * 4);
+    return (int)p->gop.size();
+}
+extern "C" void mp2vg_parsed_free(mp2vg_parsed_t* p) { delete p; }

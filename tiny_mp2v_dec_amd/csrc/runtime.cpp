@@ -1,0 +1,362 @@
+// runtime.cpp — device context of the C ABI: frame pool in HBM, resident record batch, the
+// dependency-level scheduler (one kernel launch per level), timing, downloads and digests.
+//
+// Replaces the reference's frame pool + task DAG (decoder.cpp:381-406, threads.cpp:22-211): a
+// picture's slices become workgroups; pictures whose references are complete run together in
+// one launch, so a batch of closed GOPs needs only as many launches as its longest
+// I->P->...->B chain.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "recon_kernel.h"
+#include "syntax.h"
+
+namespace mp2vg {
+hipError_t launch_recon(int cf, const KArgs& a, hipStream_t stream);
+hipError_t launch_digest(const uint8_t* pool, uint64_t slot_bytes, const int32_t* d_slots, int n,
+                         const uint64_t off[3], const int32_t stride[3], const int32_t w[3],
+                         const int32_t h[3], unsigned long long* d_out, hipStream_t stream);
+}  // namespace mp2vg
+
+using namespace mp2vg;
+
+#define HIPCHK(expr)                                                                       \
+    do {                                                                                   \
+        hipError_t e_ = (expr);                                                            \
+        if (e_ != hipSuccess) {                                                            \
+            set_error(std::string(#expr) + ": " + hipGetErrorString(e_));                  \
+            return MP2VG_E_HIP;                                                            \
+        }                                                                                  \
+    } while (0)
+
+static constexpr size_t kPoolPad = 4096;       // slack after the last slot (load5 reads 4 B past)
+static constexpr size_t kStageBytes = 32u << 20;
+
+struct mp2vg_ctx {
+    mp2vg_config_t cfg{};
+    Geom g{};
+    hipStream_t stream = nullptr;
+    uint8_t* d_pool = nullptr;
+    int32_t nslots = 0;
+
+    mp2vg_picture_t* d_pics = nullptr;
+    size_t cap_pics = 0;
+    mp2vg_mb_t* d_mbs = nullptr;
+    size_t cap_mbs = 0;
+    uint32_t* d_coefs = nullptr;
+    size_t cap_coefs = 0;
+    SliceDesc* d_slices = nullptr;
+    size_t cap_slices = 0;
+    std::vector<uint32_t> level_begin;  // slice ranges per dependency level
+    bool batch_ready = false;
+    int32_t batch_pics = 0;
+
+    std::vector<hipEvent_t> ev;  // 2 per launch
+    int nlaunch = 0;
+
+    void* h_stage = nullptr;
+    int32_t* d_dslots = nullptr;
+    unsigned long long* d_digest = nullptr;
+    size_t cap_digest = 0;
+};
+
+template <class T>
+static int grow(T*& p, size_t& cap, size_t n) {
+    if (n <= cap) return MP2VG_OK;
+    if (p) HIPCHK(hipFree(p));
+    p = nullptr;
+    size_t c = std::max(n, cap * 3 / 2);
+    HIPCHK(hipMalloc((void**)&p, c * sizeof(T)));
+    cap = c;
+    return MP2VG_OK;
+}
+
+static int upload(mp2vg_ctx_t* ctx, void* dst, const void* src, size_t bytes) {
+    const uint8_t* s = (const uint8_t*)src;
+    uint8_t* d = (uint8_t*)dst;
+    while (bytes) {
+        size_t n = std::min(bytes, kStageBytes);
+        memcpy(ctx->h_stage, s, n);
+        HIPCHK(hipMemcpyAsync(d, ctx->h_stage, n, hipMemcpyHostToDevice, ctx->stream));
+        HIPCHK(hipStreamSynchronize(ctx->stream));
+        s += n;
+        d += n;
+        bytes -= n;
+    }
+    return MP2VG_OK;
+}
+
+extern "C" int mp2vg_create(const mp2vg_config_t* cfg, mp2vg_ctx_t** out) {
+    if (!cfg || !out) return MP2VG_E_INVALID;
+    *out = nullptr;
+    if (mp2vg_frame_geometry(cfg, nullptr, nullptr, nullptr, nullptr) != MP2VG_OK) return MP2VG_E_INVALID;
+    int ndev = 0;
+    HIPCHK(hipGetDeviceCount(&ndev));
+    if (cfg->device < 0 || cfg->device >= ndev) {
+        set_error("no such HIP device");
+        return MP2VG_E_HIP;
+    }
+    HIPCHK(hipSetDevice(cfg->device));
+    mp2vg_ctx_t* c = new mp2vg_ctx_t();
+    c->cfg = *cfg;
+    c->g.init(cfg->width, cfg->height, cfg->chroma_format);
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipHostMalloc(&c->h_stage, kStageBytes, hipHostMallocDefault) != hipSuccess) {
+        set_error("stream / pinned staging allocation failed");
+        delete c;
+        return MP2VG_E_HIP;
+    }
+    int rc = mp2vg_reserve_slots(c, std::max(1, cfg->pictures_pool_size));
+    if (rc != MP2VG_OK) {
+        mp2vg_destroy(c);
+        return rc;
+    }
+    *out = c;
+    return MP2VG_OK;
+}
+
+extern "C" int mp2vg_destroy(mp2vg_ctx_t* c) {
+    if (!c) return MP2VG_E_INVALID;
+    hipSetDevice(c->cfg.device);
+    if (c->stream) hipStreamSynchronize(c->stream);
+    for (auto e : c->ev) hipEventDestroy(e);
+    hipFree(c->d_pool);
+    hipFree(c->d_pics);
+    hipFree(c->d_mbs);
+    hipFree(c->d_coefs);
+    hipFree(c->d_slices);
+    hipFree(c->d_dslots);
+    hipFree(c->d_digest);
+    if (c->h_stage) hipHostFree(c->h_stage);
+    if (c->stream) hipStreamDestroy(c->stream);
+    delete c;
+    return MP2VG_OK;
+}
+
+extern "C" int mp2vg_reserve_slots(mp2vg_ctx_t* c, int32_t nslots) {
+    if (!c || nslots <= 0) return MP2VG_E_INVALID;
+    HIPCHK(hipSetDevice(c->cfg.device));
+    if (nslots <= c->nslots) return MP2VG_OK;
+    HIPCHK(hipStreamSynchronize(c->stream));
+    uint8_t* p = nullptr;
+    size_t bytes = (size_t)c->g.slot_bytes * nslots + kPoolPad;
+    HIPCHK(hipMalloc((void**)&p, bytes));
+    HIPCHK(hipMemsetAsync(p, 0, bytes, c->stream));
+    if (c->d_pool) {
+        HIPCHK(hipMemcpyAsync(p, c->d_pool, (size_t)c->g.slot_bytes * c->nslots, hipMemcpyDeviceToDevice,
+                              c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        HIPCHK(hipFree(c->d_pool));
+    }
+    HIPCHK(hipStreamSynchronize(c->stream));
+    c->d_pool = p;
+    c->nslots = nslots;
+    return MP2VG_OK;
+}
+
+// Validate the batch so no kernel access can leave its buffers, and compute dependency levels.
+static int plan_batch(mp2vg_ctx_t* c, const mp2vg_picture_t* pics, int32_t npics, const mp2vg_mb_t* mbs,
+                      uint64_t nmbs, uint64_t ncoefs, std::vector<SliceDesc>& slices,
+                      std::vector<uint32_t>& level_begin) {
+    const int mbw = c->cfg.width / 16, mbh = c->cfg.height / 16;
+    const int nb = c->g.nblocks;
+    std::vector<int> level(npics, 0);
+    std::vector<int> last_write(c->nslots, -1), max_read(c->nslots, -1);
+    int maxlevel = -1;
+    for (int p = 0; p < npics; p++) {
+        const mp2vg_picture_t& P = pics[p];
+        if (P.mb_width != mbw || P.mb_height != mbh) {
+            set_error("picture size differs from the context geometry");
+            return MP2VG_E_INVALID;
+        }
+        if (P.dst_slot < 0 || P.dst_slot >= c->nslots || P.fwd_slot >= c->nslots || P.bwd_slot >= c->nslots) {
+            set_error("frame slot out of range (mp2vg_reserve_slots)");
+            return MP2VG_E_INVALID;
+        }
+        uint64_t nm = (uint64_t)mbw * mbh;
+        if ((uint64_t)P.mb_first + nm > nmbs) {
+            set_error("picture MB range outside the batch");
+            return MP2VG_E_INVALID;
+        }
+        bool uses[2] = {false, false};
+        for (uint64_t k = 0; k < nm; k++) {
+            const mp2vg_mb_t& m = mbs[P.mb_first + k];
+            if (m.x != k % mbw || m.y != k / mbw) {
+                set_error("MB records not in raster order");
+                return MP2VG_E_INVALID;
+            }
+            if ((uint64_t)m.coef_off + m.ncoef > ncoefs) {
+                set_error("MB coefficient range outside the batch");
+                return MP2VG_E_INVALID;
+            }
+            if (m.cbp >> nb) {
+                set_error("cbp names a block the chroma format does not have");
+                return MP2VG_E_INVALID;
+            }
+            if (!(m.flags & MP2VG_MB_INTRA)) {
+                bool f = (m.flags & MP2VG_MB_FWD) || !(m.flags & MP2VG_MB_BWD);
+                bool b = m.flags & MP2VG_MB_BWD;
+                uses[0] |= f;
+                uses[1] |= b;
+            }
+        }
+        if ((uses[0] && P.fwd_slot < 0) || (uses[1] && P.bwd_slot < 0)) {
+            set_error("picture predicts from a missing reference slot");
+            return MP2VG_E_INVALID;
+        }
+        int lv = 0;
+        if (uses[0]) lv = std::max(lv, last_write[P.fwd_slot] + 1);
+        if (uses[1]) lv = std::max(lv, last_write[P.bwd_slot] + 1);
+        lv = std::max(lv, last_write[P.dst_slot] + 1);  // WAW
+        lv = std::max(lv, max_read[P.dst_slot] + 1);    // WAR
+        if ((uses[0] && P.fwd_slot == P.dst_slot) || (uses[1] && P.bwd_slot == P.dst_slot)) {
+            set_error("picture predicts from its own slot");
+            return MP2VG_E_INVALID;
+        }
+        level[p] = lv;
+        if (uses[0]) max_read[P.fwd_slot] = std::max(max_read[P.fwd_slot], lv);
+        if (uses[1]) max_read[P.bwd_slot] = std::max(max_read[P.bwd_slot], lv);
+        last_write[P.dst_slot] = lv;
+        max_read[P.dst_slot] = -1;
+        maxlevel = std::max(maxlevel, lv);
+    }
+    level_begin.assign(maxlevel + 2, 0);
+    std::vector<std::vector<int>> bylevel(maxlevel + 1);
+    for (int p = 0; p < npics; p++) bylevel[level[p]].push_back(p);
+    slices.clear();
+    for (int L = 0; L <= maxlevel; L++) {
+        level_begin[L] = (uint32_t)slices.size();
+        for (int p : bylevel[L])
+            for (int r = 0; r < mbh; r++) slices.push_back({(uint32_t)p, pics[p].mb_first + (uint32_t)(r * mbw), (uint32_t)mbw, 0});
+    }
+    level_begin[maxlevel + 1] = (uint32_t)slices.size();
+    return MP2VG_OK;
+}
+
+extern "C" int mp2vg_batch_upload(mp2vg_ctx_t* c, const mp2vg_picture_t* pics, int32_t npics,
+                                  const mp2vg_mb_t* mbs, uint64_t nmbs, const uint32_t* coefs,
+                                  uint64_t ncoefs) {
+    if (!c || !pics || npics <= 0 || !mbs || (!coefs && ncoefs)) return MP2VG_E_INVALID;
+    HIPCHK(hipSetDevice(c->cfg.device));
+    c->batch_ready = false;
+    std::vector<SliceDesc> slices;
+    std::vector<uint32_t> lb;
+    int rc = plan_batch(c, pics, npics, mbs, nmbs, ncoefs, slices, lb);
+    if (rc != MP2VG_OK) return rc;
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if ((rc = grow(c->d_pics, c->cap_pics, (size_t)npics)) != MP2VG_OK) return rc;
+    if ((rc = grow(c->d_mbs, c->cap_mbs, (size_t)nmbs)) != MP2VG_OK) return rc;
+    if ((rc = grow(c->d_coefs, c->cap_coefs, (size_t)std::max<uint64_t>(ncoefs, 1))) != MP2VG_OK) return rc;
+    if ((rc = grow(c->d_slices, c->cap_slices, slices.size())) != MP2VG_OK) return rc;
+    if ((rc = upload(c, c->d_pics, pics, sizeof(mp2vg_picture_t) * npics)) != MP2VG_OK) return rc;
+    if ((rc = upload(c, c->d_mbs, mbs, sizeof(mp2vg_mb_t) * nmbs)) != MP2VG_OK) return rc;
+    if (ncoefs && (rc = upload(c, c->d_coefs, coefs, sizeof(uint32_t) * ncoefs)) != MP2VG_OK) return rc;
+    if ((rc = upload(c, c->d_slices, slices.data(), sizeof(SliceDesc) * slices.size())) != MP2VG_OK) return rc;
+    c->level_begin = lb;
+    c->batch_pics = npics;
+    c->batch_ready = true;
+    return MP2VG_OK;
+}
+
+extern "C" int mp2vg_batch_decode(mp2vg_ctx_t* c) {
+    if (!c) return MP2VG_E_INVALID;
+    if (!c->batch_ready) {
+        set_error("no batch uploaded");
+        return MP2VG_E_STATE;
+    }
+    HIPCHK(hipSetDevice(c->cfg.device));
+    int nl = (int)c->level_begin.size() - 1;
+    while ((int)c->ev.size() < 2 * nl) {
+        hipEvent_t e;
+        HIPCHK(hipEventCreate(&e));
+        c->ev.push_back(e);
+    }
+    KArgs a;
+    memset(&a, 0, sizeof a);
+    a.pics = c->d_pics;
+    a.mbs = c->d_mbs;
+    a.coefs = c->d_coefs;
+    a.slices = c->d_slices;
+    a.pool = c->d_pool;
+    a.slot_bytes = c->g.slot_bytes;
+    for (int i = 0; i < 3; i++) {
+        a.plane_off[i] = c->g.plane_off[i];
+        a.stride[i] = c->g.stride[i];
+        a.ph[i] = c->g.ph[i];
+    }
+    for (int L = 0; L < nl; L++) {
+        a.slice_base = c->level_begin[L];
+        a.nslices = c->level_begin[L + 1] - c->level_begin[L];
+        HIPCHK(hipEventRecord(c->ev[2 * L], c->stream));
+        if (a.nslices) HIPCHK(launch_recon(c->g.cf, a, c->stream));
+        HIPCHK(hipEventRecord(c->ev[2 * L + 1], c->stream));
+    }
+    c->nlaunch = nl;
+    return MP2VG_OK;
+}
+
+extern "C" int mp2vg_synchronize(mp2vg_ctx_t* c) {
+    if (!c) return MP2VG_E_INVALID;
+    HIPCHK(hipSetDevice(c->cfg.device));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return MP2VG_OK;
+}
+
+extern "C" int mp2vg_last_launch_times(mp2vg_ctx_t* c, float* ms, int32_t max, int32_t* count) {
+    if (!c) return MP2VG_E_INVALID;
+    HIPCHK(hipSetDevice(c->cfg.device));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (count) *count = c->nlaunch;
+    for (int i = 0; i < c->nlaunch && i < max; i++) HIPCHK(hipEventElapsedTime(&ms[i], c->ev[2 * i], c->ev[2 * i + 1]));
+    return MP2VG_OK;
+}
+
+extern "C" int mp2vg_download_slot(mp2vg_ctx_t* c, int32_t slot, uint8_t* dst[3], const int32_t dst_stride[3]) {
+    if (!c || !dst || slot < 0 || slot >= c->nslots) return MP2VG_E_INVALID;
+    HIPCHK(hipSetDevice(c->cfg.device));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    for (int p = 0; p < 3; p++) {
+        size_t ds = (dst_stride && dst_stride[p]) ? (size_t)dst_stride[p] : (size_t)c->g.pw[p];
+        const uint8_t* src = c->d_pool + (size_t)slot * c->g.slot_bytes + c->g.plane_off[p];
+        HIPCHK(hipMemcpy2DAsync(dst[p], ds, src, c->g.stride[p], c->g.pw[p], c->g.ph[p], hipMemcpyDeviceToHost,
+                                c->stream));
+    }
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return MP2VG_OK;
+}
+
+extern "C" int mp2vg_slot_device_ptr(mp2vg_ctx_t* c, int32_t slot, void** dptr) {
+    if (!c || !dptr || slot < 0 || slot >= c->nslots) return MP2VG_E_INVALID;
+    *dptr = c->d_pool + (size_t)slot * c->g.slot_bytes;
+    return MP2VG_OK;
+}
+
+extern "C" int mp2vg_slot_digests(mp2vg_ctx_t* c, const int32_t* slots, int32_t n, uint64_t* out) {
+    if (!c || !slots || !out || n <= 0) return MP2VG_E_INVALID;
+    for (int i = 0; i < n; i++)
+        if (slots[i] < 0 || slots[i] >= c->nslots) return MP2VG_E_INVALID;
+    HIPCHK(hipSetDevice(c->cfg.device));
+    if ((size_t)n > c->cap_digest) {
+        hipFree(c->d_dslots);
+        hipFree(c->d_digest);
+        c->d_dslots = nullptr;
+        c->d_digest = nullptr;
+        HIPCHK(hipMalloc((void**)&c->d_dslots, sizeof(int32_t) * n));
+        HIPCHK(hipMalloc((void**)&c->d_digest, sizeof(unsigned long long) * n));
+        c->cap_digest = n;
+    }
+    HIPCHK(hipMemcpyAsync(c->d_dslots, slots, sizeof(int32_t) * n, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemsetAsync(c->d_digest, 0, sizeof(unsigned long long) * n, c->stream));
+    int32_t st[3] = {c->g.stride[0], c->g.stride[1], c->g.stride[2]};
+    int32_t w[3] = {c->g.pw[0], c->g.pw[1], c->g.pw[2]};
+    int32_t h[3] = {c->g.ph[0], c->g.ph[1], c->g.ph[2]};
+    HIPCHK(launch_digest(c->d_pool, c->g.slot_bytes, c->d_dslots, n, c->g.plane_off, st, w, h, c->d_digest, c->stream));
+    HIPCHK(hipMemcpyAsync(out, c->d_digest, sizeof(uint64_t) * n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return MP2VG_OK;
+}

@@ -1,0 +1,230 @@
+// syntax.h — host-side MPEG-2 syntax helpers shared by the record emitter (parse.cpp) and the
+// synthetic stream writer (gen.cpp): bit reader/writer, VLC LUTs, and the small pieces of the
+// reference's parse semantics both must agree on (qscale mapping, MV prediction, W build, MC
+// read extents).
+#pragma once
+#include <cstdint>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/mp2vg.h"
+#include "vlc_tables.h"
+
+namespace mp2vg {
+
+// ---------------------------------------------------------------------------------------------
+// MSB-first bit reader over a byte buffer (zeros past the end).  Plays the role of the
+// reference's bitstream_reader_c (bitstream.h:22-64); peek(n) for n <= 32.
+struct BitReader {
+    const uint8_t* base = nullptr;
+    const uint8_t* p = nullptr;
+    const uint8_t* end = nullptr;
+    uint64_t cache = 0;
+    int bits = 0;  // valid bits in cache (MSB aligned)
+
+    BitReader() = default;
+    BitReader(const uint8_t* b, const uint8_t* e) : base(b), p(b), end(e) {}
+
+    inline void refill() {
+        while (bits <= 56) {
+            uint64_t byte = (p < end) ? *p : 0;
+            cache |= byte << (56 - bits);
+            p++;
+            bits += 8;
+        }
+    }
+    inline uint32_t peek(int n) {
+        if (n == 0) return 0;
+        refill();
+        return (uint32_t)(cache >> (64 - n));
+    }
+    inline void skip(int n) {
+        refill();
+        cache <<= n;
+        bits -= n;
+    }
+    inline uint32_t read(int n) {
+        uint32_t v = peek(n);
+        if (n) skip(n);
+        return v;
+    }
+    uint64_t bitpos() const { return (uint64_t)(p - base) * 8 - bits; }
+    bool overrun() const { return p > end + 8; }
+};
+
+// MSB-first bit writer
+struct BitWriter {
+    std::vector<uint8_t> out;
+    uint64_t acc = 0;
+    int nacc = 0;
+
+    void put(uint32_t value, int n) {
+        for (int i = n - 1; i >= 0; i--) {
+            acc = (acc << 1) | ((value >> i) & 1u);
+            if (++nacc == 8) {
+                out.push_back((uint8_t)acc);
+                acc = 0;
+                nacc = 0;
+            }
+        }
+    }
+    void put_code(const char* bits) {
+        for (const char* c = bits; *c; c++) put(*c == '1', 1);
+    }
+    void align() {  // zero stuffing to the next byte boundary
+        while (nacc) put(0, 1);
+    }
+    void start_code(uint8_t code) {
+        align();
+        out.push_back(0);
+        out.push_back(0);
+        out.push_back(1);
+        out.push_back(code);
+    }
+};
+
+// ---------------------------------------------------------------------------------------------
+// VLC decode LUT built from a code list: lut[peek(maxlen)] = {len, index}.
+struct VlcLut {
+    int maxlen = 0;
+    std::vector<uint32_t> lut;  // (len << 16) | (index + 1), 0 = invalid
+
+    void add(const char* bits, int index) {
+        int len = (int)strlen(bits);
+        uint32_t code = 0;
+        for (int i = 0; i < len; i++) code = (code << 1) | (bits[i] == '1');
+        uint32_t lo = code << (maxlen - len), hi = (code + 1) << (maxlen - len);
+        for (uint32_t v = lo; v < hi; v++) lut[v] = ((uint32_t)len << 16) | (uint32_t)(index + 1);
+    }
+    void init(int ml) {
+        maxlen = ml;
+        lut.assign(1u << ml, 0);
+    }
+    // returns index or -1; consumes the code
+    inline int decode(BitReader& br) const {
+        uint32_t e = lut[br.peek(maxlen)];
+        if (!e) return -1;
+        br.skip((int)(e >> 16));
+        return (int)(e & 0xffff) - 1;
+    }
+};
+
+struct Tables {
+    VlcLut mba, mbtype[4], cbp, motion, dc_luma, dc_chroma, coef[2];
+    // coefficient LUT payload: index into run/level arrays; special indices
+    enum { COEF_EOB = 1000, COEF_ESC = 1001 };
+    std::vector<int> coef_run[2], coef_level[2];
+    static const Tables& get();
+};
+
+// ---------------------------------------------------------------------------------------------
+// Reference parse semantics shared by emitter and writer.
+
+// quantiser_scale from quantiser_scale_code (decoder.cpp:140-145, mb_decoder.cpp:555-563)
+inline int qscale_from_code(int code, int q_scale_type) {
+    if (!q_scale_type) return code << 1;
+    if (code < 9) return code;
+    if (code < 17) return (code - 4) << 1;
+    if (code < 25) return (code - 10) << 2;
+    return (code - 17) << 3;
+}
+
+// update_motion_predictor (mb_decoder.cpp:447-477) for one component.
+// field_vert: mv_format == Field && t == 1 in a frame picture.
+inline int16_t mv_reconstruct(int f_code, int motion_code, int residual, int16_t& PMV, bool field_vert) {
+    int r_size = f_code - 1;
+    int f = 1 << r_size;
+    int high = 16 * f - 1, low = -16 * f, range = 32 * f;
+    int delta;
+    if (f != 1 && motion_code != 0) {
+        delta = ((motion_code < 0 ? -motion_code : motion_code) - 1) * f + residual + 1;
+        if (motion_code < 0) delta = -delta;
+    } else {
+        delta = motion_code;
+    }
+    int prediction = field_vert ? (PMV >> 1) : PMV;
+    int mv = prediction + delta;
+    if (mv < low) mv += range;
+    if (mv > high) mv -= range;
+    int16_t MV = (int16_t)mv;
+    PMV = field_vert ? (int16_t)(MV * 2) : MV;
+    return MV;
+}
+
+// W[k][scan i] from quant_matrix_extension matrices (transmitted in zig-zag order)
+// (decoder.cpp:154-192: tmp = raster via g_scan[0]; W = tmp[g_shuffle[alt][i]]).
+extern const uint8_t kScanRaster[2][64];  // scan position -> raster index (v*8+u)
+inline void build_W(const uint8_t qme[4][64], int alt, uint8_t W[4][64]) {
+    uint8_t zz_of_raster[64];
+    for (int zz = 0; zz < 64; zz++) zz_of_raster[kScanRaster[0][zz]] = (uint8_t)zz;
+    for (int k = 0; k < 4; k++)
+        for (int i = 0; i < 64; i++) W[k][i] = qme[k][zz_of_raster[kScanRaster[alt][i]]];
+}
+
+// Frame geometry (decoder.cpp:44-68)
+struct Geom {
+    int cf;
+    int pw[3], ph[3], stride[3];
+    uint64_t plane_off[3], slot_bytes;
+    int mbw_c, mbh_c;  // chroma MB size
+    int nblocks;
+    void init(int width, int height, int chroma_format) {
+        cf = chroma_format;
+        stride[0] = (width + 63) & ~63;
+        pw[0] = width;
+        ph[0] = height;
+        if (cf == 3) {
+            stride[1] = stride[0];
+            pw[1] = width;
+            ph[1] = height;
+        } else {
+            stride[1] = ((stride[0] >> 1) + 63) & ~63;
+            pw[1] = width >> 1;
+            ph[1] = cf == 1 ? height >> 1 : height;
+        }
+        stride[2] = stride[1];
+        pw[2] = pw[1];
+        ph[2] = ph[1];
+        plane_off[0] = 0;
+        plane_off[1] = (uint64_t)stride[0] * ph[0];
+        plane_off[2] = plane_off[1] + (uint64_t)stride[1] * ph[1];
+        slot_bytes = plane_off[2] + (uint64_t)stride[2] * ph[2];
+        mbw_c = cf == 3 ? 16 : 8;
+        mbh_c = cf == 1 ? 8 : 16;
+        nblocks = cf == 1 ? 6 : (cf == 2 ? 8 : 12);
+    }
+};
+
+// Do the reference's MC reads for one vector of one direction stay inside every plane?
+// (mb_decoder.cpp:212-289 address arithmetic; SSE2 loads read width(+1 if x half-pel) bytes and
+// height(+1 row-step if y half-pel) rows.)
+inline bool mc_reads_inside(const Geom& g, int mbx, int mby, int mvx, int mvy, bool field, int fs, int r) {
+    for (int plane = 0; plane < 3; plane++) {
+        int mx = mvx, my = mvy;
+        if (plane > 0) {
+            if (g.cf < 3) mx >>= 1;
+            if (g.cf < 2) my >>= 1;
+        }
+        int w = plane == 0 ? 16 : g.mbw_c;
+        int h = plane == 0 ? 16 : g.mbh_c;
+        int x0 = mbx * w + (mx >> 1);
+        int x1 = x0 + w - 1 + (mx & 1);
+        int y0, y1;
+        if (!field) {
+            y0 = mby * h + (my >> 1);
+            y1 = y0 + h - 1 + (my & 1);
+        } else {
+            int hf = h >> 1;
+            y0 = mby * h + fs + 2 * (my >> 1);
+            y1 = y0 + 2 * (hf - 1) + 2 * (my & 1);
+        }
+        (void)r;
+        if (x0 < 0 || y0 < 0 || x1 > g.pw[plane] - 1 || y1 > g.ph[plane] - 1) return false;
+    }
+    return true;
+}
+
+void set_error(const std::string& msg);
+
+}  // namespace mp2vg

@@ -1,0 +1,150 @@
+"""Host side of the record path: stream generation, ES -> records parsing, and the device
+context (frame pool + record batch + level-scheduled launches), mirroring the reference's
+mp2v_decoder_c / frame_c vocabulary where it has one.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import MB_DTYPE, PIC_DTYPE, check, lib
+
+
+def gen_params(**kw):
+    p = _lib.GenParams()
+    lib().mp2vg_gen_default_params(ctypes.byref(p))
+    for k, v in kw.items():
+        if not hasattr(p, k):
+            raise KeyError(k)
+        setattr(p, k, v)
+    return p
+
+
+def generate_es(**kw):
+    """Write a synthetic elementary stream of the reference's decodable subset (bytes)."""
+    p = gen_params(**kw)
+    ptr, n = ctypes.c_void_p(), ctypes.c_uint64()
+    check(lib().mp2vg_generate_es(ctypes.byref(p), ctypes.byref(ptr), ctypes.byref(n)), "generate_es")
+    try:
+        return ctypes.string_at(ptr, n.value)
+    finally:
+        lib().mp2vg_free(ptr)
+
+
+class Parsed:
+    """Records of a whole elementary stream (pictures in decode order; slot = decode index)."""
+
+    def __init__(self, es: bytes, width, height, chroma_format, threads=0, reordering=True):
+        self.width, self.height, self.chroma_format = width, height, chroma_format
+        cfg = _lib.make_config(width, height, chroma_format, threads=threads, reordering=reordering)
+        buf = np.frombuffer(es + b"\0" * 64, dtype=np.uint8)
+        h = ctypes.c_void_p()
+        check(lib().mp2vg_parse_es(buf.ctypes.data_as(ctypes.c_void_p), len(es), ctypes.byref(cfg),
+                                   ctypes.byref(h)), "parse_es")
+        try:
+            npics, nmbs, ncoefs = ctypes.c_int32(), ctypes.c_uint64(), ctypes.c_uint64()
+            lib().mp2vg_parsed_counts(h, ctypes.byref(npics), ctypes.byref(nmbs), ctypes.byref(ncoefs))
+            n, m, c = npics.value, nmbs.value, ncoefs.value
+            self.pics = np.frombuffer(ctypes.string_at(lib().mp2vg_parsed_pictures(h), n * 288), PIC_DTYPE).copy()
+            self.mbs = np.frombuffer(ctypes.string_at(lib().mp2vg_parsed_mbs(h), m * 32), MB_DTYPE).copy()
+            self.coefs = (np.frombuffer(ctypes.string_at(lib().mp2vg_parsed_coefs(h), c * 4), np.uint32).copy()
+                          if c else np.zeros(0, np.uint32))
+            order = (ctypes.c_int32 * max(n, 1))()
+            lib().mp2vg_parsed_display_order(h, order, n)
+            self.display = np.array(order[:n], dtype=np.int32)
+            gop = (ctypes.c_int32 * max(n, 1))()
+            lib().mp2vg_parsed_gop_index(h, gop, n)
+            self.gop = np.array(gop[:n], dtype=np.int32)
+        finally:
+            lib().mp2vg_parsed_free(h)
+
+    @property
+    def npics(self):
+        return len(self.pics)
+
+
+class DeviceContext:
+    """mp2vg_ctx_t: a frame pool in HBM plus a resident record batch on one GPU."""
+
+    def __init__(self, width, height, chroma_format, slots, device=0):
+        self.width, self.height, self.chroma_format = width, height, chroma_format
+        self.cfg = _lib.make_config(width, height, chroma_format, pool=slots, device=device)
+        self.h = ctypes.c_void_p()
+        check(lib().mp2vg_create(ctypes.byref(self.cfg), ctypes.byref(self.h)), "create")
+        self.pw, self.ph, self.stride, self.slot_bytes = _lib.geometry(width, height, chroma_format)
+        self.nslots = slots
+
+    def close(self):
+        if self.h:
+            lib().mp2vg_destroy(self.h)
+            self.h = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def reserve(self, slots):
+        check(lib().mp2vg_reserve_slots(self.h, slots), "reserve_slots")
+        self.nslots = max(self.nslots, slots)
+
+    def upload(self, pics, mbs, coefs):
+        pics = np.ascontiguousarray(pics, PIC_DTYPE)
+        mbs = np.ascontiguousarray(mbs, MB_DTYPE)
+        coefs = np.ascontiguousarray(coefs, np.uint32)
+        vp = ctypes.c_void_p
+        check(lib().mp2vg_batch_upload(self.h, pics.ctypes.data_as(vp), len(pics), mbs.ctypes.data_as(vp), len(mbs),
+                                       coefs.ctypes.data_as(vp) if len(coefs) else None, len(coefs)), "batch_upload")
+
+    def decode(self):
+        check(lib().mp2vg_batch_decode(self.h), "batch_decode")
+
+    def synchronize(self):
+        check(lib().mp2vg_synchronize(self.h), "synchronize")
+
+    def launch_times_ms(self):
+        buf = (ctypes.c_float * 256)()
+        n = ctypes.c_int32()
+        check(lib().mp2vg_last_launch_times(self.h, buf, 256, ctypes.byref(n)), "last_launch_times")
+        return list(buf[:min(n.value, 256)])
+
+    def download(self, slot):
+        """Visible planes of one slot: [Y, U, V] numpy arrays (height x width)."""
+        planes = [np.empty((self.ph[i], self.pw[i]), np.uint8) for i in range(3)]
+        ptrs = (ctypes.c_void_p * 3)(*[p.ctypes.data for p in planes])
+        check(lib().mp2vg_download_slot(self.h, slot, ptrs, None), "download_slot")
+        return planes
+
+    def digests(self, slots):
+        slots = np.ascontiguousarray(slots, np.int32)
+        out = np.zeros(len(slots), np.uint64)
+        check(lib().mp2vg_slot_digests(self.h, slots.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), len(slots),
+                                       out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))), "slot_digests")
+        return out
+
+
+def frame_yuv_bytes(planes):
+    """The reference sample's write_yuv layout (tiny_mp2v_dec.cpp:11-17): Y, U, V rows of width."""
+    return b"".join(np.ascontiguousarray(p).tobytes() for p in planes)
+
+
+def planes_digest(planes):
+    """Host twin of the device digest: sum_rows fnv1a64(row) * (2*row_id + 1) mod 2^64."""
+    total = 0
+    rid = 0
+    for p in planes:
+        for row in np.asarray(p):
+            h = 1469598103934665603
+            for b in row.tobytes():
+                h ^= b
+                h = (h * 1099511628211) & 0xFFFFFFFFFFFFFFFF
+            total = (total + h * (2 * rid + 1)) & 0xFFFFFFFFFFFFFFFF
+            rid += 1
+    return total
