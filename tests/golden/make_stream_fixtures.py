@@ -1,0 +1,96 @@
+"""Generate the whole-stream golden fixtures from the REAL reference decoder.
+
+Run in the build container (needs oracle/_ref/ref_decode, built from /root/reference by
+`make -C oracle ref`).  For every case below: write the elementary stream with our stream
+writer (accepted subset only), decode it with the compiled reference at 1 and 4
+threads (outputs must agree), and store
+  tests/golden/streams/<name>.m2v           the input stream
+  tests/golden/streams/manifest.json        geometry + per-frame MD5 of the reference's YUV
+                                            output in display order (reference
+                                            tiny_mp2v_dec.cpp:11-17 write_yuv layout)
+The reference itself does not travel to the GPU box; these files do.
+"""
+import hashlib
+import json
+import os
+import subprocess
+import sys
+import tempfile
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, REPO)
+REF = os.path.join(REPO, "oracle", "_ref", "ref_decode")
+OUT = os.path.join(HERE, "streams")
+
+from tiny_mp2v_dec_amd.records import generate_es  # noqa: E402
+
+CASES = [
+    # name, width, height, chroma_format, generator params
+    ("i420_cif_intra", 352, 288, 1, dict(n_gops=1, gop_n=3, gop_m=1, mix=1, seed=1729)),
+    ("ipb420_qcif", 176, 144, 1, dict(n_gops=2, gop_n=12, gop_m=3, leading_b=1, seed=1730)),
+    ("ipb420_qcif_openb", 176, 144, 1, dict(n_gops=1, gop_n=10, gop_m=3, leading_b=0, seed=1731)),
+    ("ipb420_field", 176, 144, 1, dict(n_gops=1, gop_n=12, gop_m=3, frame_pred_frame_dct=0, seed=1732)),
+    ("ipb422_qcif", 176, 144, 2, dict(n_gops=1, gop_n=12, gop_m=3, seed=1733)),
+    ("ipb422_field", 176, 144, 2, dict(n_gops=1, gop_n=12, gop_m=3, frame_pred_frame_dct=0, seed=1734)),
+    ("ipb444_qcif", 176, 144, 3, dict(n_gops=1, gop_n=12, gop_m=3, seed=1735)),
+    ("stress_saturation", 352, 288, 1, dict(n_gops=1, gop_n=9, gop_m=2, frame_pred_frame_dct=0,
+                                            big_level_permille=250, escape_permille=300,
+                                            big_matrix_permille=400, coefs_max=30, intra_coefs_max=50,
+                                            seed=1736)),
+    ("stress_mv_fcode4", 352, 288, 2, dict(n_gops=1, gop_n=9, gop_m=3, f_code=4, quant_permille=400,
+                                           frame_pred_frame_dct=0, seed=1737)),
+    ("mc_heavy_fcode1", 176, 144, 1, dict(n_gops=1, gop_n=12, gop_m=3, f_code=1, mix=2, seed=1738)),
+    ("tall_2816_vpos_ext", 64, 2816, 1, dict(n_gops=1, gop_n=4, gop_m=3, leading_b=0, seed=1739)),
+    ("hd1080_420_ipb", 1920, 1088, 1, dict(n_gops=1, gop_n=4, gop_m=3, leading_b=0, seed=1740)),
+]
+
+
+def ref_decode(path, w, h, cf, threads, out):
+    r = subprocess.run([REF, path, str(w), str(h), str(cf), str(threads), out], capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"reference failed on {path}: {r.returncode} {r.stderr[-400:]}")
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+def main():
+    if not os.path.exists(REF):
+        sys.exit("build the reference first: make -C oracle ref")
+    os.makedirs(OUT, exist_ok=True)
+    manifest = []
+    with tempfile.TemporaryDirectory() as tmp:
+        for name, w, h, cf, params in CASES:
+            es = generate_es(width=w, height=h, chroma_format=cf, **params)
+            path = os.path.join(OUT, name + ".m2v")
+            with open(path, "wb") as f:
+                f.write(es)
+            y1, y4 = os.path.join(tmp, "a.yuv"), os.path.join(tmp, "b.yuv")
+            # golden = the single-threaded reference; the multi-threaded reference is checked
+            # against it (its busy-spin task queue, threads.cpp:108-159, is racy: a rare
+            # mismatch is recorded, not hidden)
+            info = ref_decode(path, w, h, cf, 1, y1)
+            a = open(y1, "rb").read()
+            cw = w if cf == 3 else w // 2
+            ch = h if cf != 1 else h // 2
+            fb = w * h + 2 * cw * ch
+            assert len(a) == fb * info["frames"], name
+            md5 = [hashlib.md5(a[k * fb:(k + 1) * fb]).hexdigest() for k in range(info["frames"])]
+            mt_mismatch = []
+            for _ in range(3):
+                ref_decode(path, w, h, cf, 4, y4)
+                b = open(y4, "rb").read()
+                if b != a:
+                    md5b = [hashlib.md5(b[k * fb:(k + 1) * fb]).hexdigest() for k in range(len(b) // fb)]
+                    bad = [k for k in range(min(len(md5), len(md5b))) if md5[k] != md5b[k]]
+                    mt_mismatch.append(bad)
+                    print(f"WARNING {name}: 4-thread reference differs from 1-thread at frames {bad}")
+            manifest.append(dict(name=name, file=name + ".m2v", width=w, height=h, chroma_format=cf,
+                                 frames=info["frames"], bytes=len(es), params=params, md5=md5,
+                                 ref_mt_mismatch=mt_mismatch))
+            print(f"{name}: {info['frames']} frames, {len(es)} bytes")
+    with open(os.path.join(OUT, "manifest.json"), "w") as f:
+        json.dump(manifest, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
