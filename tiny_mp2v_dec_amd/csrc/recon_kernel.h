@@ -30,6 +30,14 @@ struct SliceDesc {
     uint32_t reserved;
 };
 
+// per-launch geometry, passed by value
+struct Geo {
+    uint64_t slot_bytes;
+    uint64_t plane_off[3];
+    int32_t stride[3];
+    int32_t ph[3];
+};
+
 struct KArgs {
     const mp2vg_picture_t* pics;
     const mp2vg_mb_t* mbs;

@@ -36,6 +36,7 @@ using namespace mp2vg;
 
 static constexpr size_t kPoolPad = 4096;       // slack after the last slot (load5 reads 4 B past)
 static constexpr size_t kStageBytes = 32u << 20;
+static constexpr size_t kMbPad = 16;  // >= the kernel's MB group size
 
 struct mp2vg_ctx {
     mp2vg_config_t cfg{};
@@ -194,6 +195,14 @@ static int plan_batch(mp2vg_ctx_t* c, const mp2vg_picture_t* pics, int32_t npics
                 set_error("MB coefficient range outside the batch");
                 return MP2VG_E_INVALID;
             }
+            // the kernel streams the coefficient words of consecutive MBs of a row as one range
+            if (k % mbw != 0) {
+                const mp2vg_mb_t& pm = mbs[P.mb_first + k - 1];
+                if ((uint64_t)pm.coef_off + pm.ncoef != m.coef_off) {
+                    set_error("coefficient words of a macroblock row are not contiguous");
+                    return MP2VG_E_INVALID;
+                }
+            }
             if (m.cbp >> nb) {
                 set_error("cbp names a block the chroma format does not have");
                 return MP2VG_E_INVALID;
@@ -250,7 +259,8 @@ extern "C" int mp2vg_batch_upload(mp2vg_ctx_t* c, const mp2vg_picture_t* pics, i
     if (rc != MP2VG_OK) return rc;
     HIPCHK(hipStreamSynchronize(c->stream));
     if ((rc = grow(c->d_pics, c->cap_pics, (size_t)npics)) != MP2VG_OK) return rc;
-    if ((rc = grow(c->d_mbs, c->cap_mbs, (size_t)nmbs)) != MP2VG_OK) return rc;
+    // the kernel reads whole MB groups with scalar loads: pad the record array
+    if ((rc = grow(c->d_mbs, c->cap_mbs, (size_t)nmbs + kMbPad)) != MP2VG_OK) return rc;
     if ((rc = grow(c->d_coefs, c->cap_coefs, (size_t)std::max<uint64_t>(ncoefs, 1))) != MP2VG_OK) return rc;
     if ((rc = grow(c->d_slices, c->cap_slices, slices.size())) != MP2VG_OK) return rc;
     if ((rc = upload(c, c->d_pics, pics, sizeof(mp2vg_picture_t) * npics)) != MP2VG_OK) return rc;

@@ -135,16 +135,24 @@ def frame_yuv_bytes(planes):
     return b"".join(np.ascontiguousarray(p).tobytes() for p in planes)
 
 
+def _mix64(z):
+    z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return z ^ (z >> np.uint64(31))
+
+
 def planes_digest(planes):
-    """Host twin of the device digest: sum_rows fnv1a64(row) * (2*row_id + 1) mod 2^64."""
-    total = 0
-    rid = 0
-    for p in planes:
-        for row in np.asarray(p):
-            h = 1469598103934665603
-            for b in row.tobytes():
-                h ^= b
-                h = (h * 1099511628211) & 0xFFFFFFFFFFFFFFFF
-            total = (total + h * (2 * rid + 1)) & 0xFFFFFFFFFFFFFFFF
-            rid += 1
-    return total
+    """Host twin of the device digest (recon.hip digest_kernel): sum over visible dwords d at
+    (row_id, byte x), rows numbered across Y, U, V, of mix64((row_id << 32) | x) ^ d, mod 2^64."""
+    total = np.uint64(0)
+    row0 = 0
+    with np.errstate(over="ignore"):
+        for p in planes:
+            p = np.ascontiguousarray(p)
+            h, w = p.shape
+            d = p.view("<u4").astype(np.uint64)  # (h, w/4)
+            rows = (np.arange(h, dtype=np.uint64) + np.uint64(row0))[:, None]
+            xs = (np.arange(w // 4, dtype=np.uint64) * np.uint64(4))[None, :]
+            total = total + np.sum(_mix64((rows << np.uint64(32)) | xs) ^ d, dtype=np.uint64)
+            row0 += h
+    return int(total)

@@ -1,0 +1,84 @@
+"""Summarise a tools/profile.sh run (gpurun_out/prof_<tag>/) for the recon kernel.
+
+    python tools/prof_summary.py <tag> [--mbs-per-launch-total N] [--out profiles/<file>.md]
+
+Prints the rocprofv3 kernel stats, per-dispatch averages of every PMC counter, and the HBM
+traffic per dispatch derived the way MI355X_MICROARCH.md prescribes (FETCH_SIZE/WRITE_SIZE are
+KiB; gfx950 FETCH_SIZE under-reports wide streaming reads by 2x, so both the raw and the x2
+value are shown).
+"""
+import argparse
+import collections
+import csv
+import os
+import statistics
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def load_counters(d, name):
+    path = os.path.join(d, name, f"{name}_counter_collection.csv")
+    if not os.path.exists(path):
+        return {}
+    per = collections.defaultdict(list)
+    for r in csv.DictReader(open(path)):
+        if "recon_kernel" not in r["Kernel_Name"]:
+            continue
+        per[r["Counter_Name"]].append(float(r["Counter_Value"]))
+    return per
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("tag")
+    ap.add_argument("--out")
+    args = ap.parse_args()
+    d = os.path.join(REPO, "gpurun_out", f"prof_{args.tag}")
+    lines = [f"# rocprofv3 summary: {args.tag}", ""]
+    stats = os.path.join(d, "ktrace", "ktrace_kernel_stats.csv")
+    if os.path.exists(stats):
+        lines.append("## kernel stats (rocprofv3 --kernel-trace --stats)")
+        lines.append("")
+        lines.append("| kernel | calls | avg ns | total ns | % |")
+        lines.append("|---|---|---|---|---|")
+        for r in csv.DictReader(open(stats)):
+            lines.append(f"| {r['Name'][:70]} | {r['Calls']} | {float(r['AverageNs']):.0f} | "
+                         f"{float(r['TotalDurationNs']):.0f} | {float(r['Percentage']):.2f} |")
+        lines.append("")
+    trace = os.path.join(d, "ktrace", "ktrace_kernel_trace.csv")
+    durs = []
+    if os.path.exists(trace):
+        for r in csv.DictReader(open(trace)):
+            if "recon_kernel" in r["Kernel_Name"]:
+                durs.append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    counters = {}
+    for name in ("fetch", "write", "sq1", "sq2", "tcc"):
+        counters.update(load_counters(d, name))
+    if counters:
+        lines.append("## PMC counters, recon_kernel, mean per dispatch")
+        lines.append("")
+        lines.append("| counter | mean per dispatch | dispatches |")
+        lines.append("|---|---|---|")
+        for k in sorted(counters):
+            v = counters[k]
+            lines.append(f"| {k} | {statistics.mean(v):.4g} | {len(v)} |")
+        lines.append("")
+        if "FETCH_SIZE" in counters and "WRITE_SIZE" in counters:
+            f = statistics.mean(counters["FETCH_SIZE"]) * 1024
+            w = statistics.mean(counters["WRITE_SIZE"]) * 1024
+            lines.append(f"HBM-side bytes per dispatch: FETCH {f / 1e6:.1f} MB raw ({2 * f / 1e6:.1f} MB with the "
+                         f"gfx950 x2 correction), WRITE {w / 1e6:.1f} MB; traffic (FETCH x2 + WRITE) "
+                         f"{(2 * f + w) / 1e6:.1f} MB")
+            if durs:
+                lines.append(f"kernel-trace mean duration {statistics.mean(durs) / 1e3:.1f} us over {len(durs)} dispatches")
+        lines.append("")
+    text = "\n".join(lines)
+    print(text)
+    if args.out:
+        with open(args.out, "w") as fh:
+            fh.write(text + "\n")
+
+
+if __name__ == "__main__":
+    sys.exit(main())
