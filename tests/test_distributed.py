@@ -1,0 +1,106 @@
+"""CPU, world_size 2 over gloo: GOP sharding + the digest gather that bench.py does over RCCL.
+
+Each rank takes GOPs g % world == rank of one stream, reconstructs its shard (here with the
+oracle, as the CPU stand-in for the HIP kernel), computes per-frame digests, and all_gathers
+them to every rank; the union must equal the single-process decode of the whole stream.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, es, q):
+    import sys
+    sys.path[:0] = [REPO, os.path.join(REPO, "tests")]
+    import torch
+    from helpers import oracle_frames
+    from tiny_mp2v_dec_amd.records import Parsed, planes_digest
+    from tiny_mp2v_dec_amd.shard import shard_batch
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    parsed = Parsed(es, 176, 144, 1)
+    pics, mbs, coefs, ids = shard_batch(parsed, rank, world)
+
+    class P:
+        pass
+
+    sp = P()
+    sp.width, sp.height, sp.chroma_format = 176, 144, 1
+    sp.pics, sp.mbs, sp.coefs, sp.npics = pics, mbs, coefs, len(pics)
+    frames = oracle_frames(sp)
+    local = torch.tensor([[int(i), planes_digest(f) - (1 << 63)] for i, f in zip(ids, frames)], dtype=torch.int64)
+    n = torch.tensor([len(local)])
+    sizes = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(sizes, n)
+    mx = int(max(s.item() for s in sizes))
+    pad = torch.full((mx, 2), -1, dtype=torch.int64)
+    pad[:len(local)] = local
+    outs = [torch.empty_like(pad) for _ in range(world)]
+    dist.all_gather(outs, pad)
+    if rank == 0:
+        got = {}
+        for o in outs:
+            for i, d in o.tolist():
+                if i >= 0:
+                    got[i] = d + (1 << 63)
+        q.put(got)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2])
+def test_gop_shard_gather_equals_single_process(world):
+    import sys
+    sys.path[:0] = [REPO, os.path.join(REPO, "tests")]
+    from helpers import oracle_frames
+    from tiny_mp2v_dec_amd.records import Parsed, generate_es, planes_digest
+
+    es = generate_es(width=176, height=144, chroma_format=1, n_gops=3, gop_n=6, gop_m=3, seed=77)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, es, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    full = Parsed(es, 176, 144, 1)
+    exp = {i: planes_digest(f) for i, f in enumerate(oracle_frames(full))}
+    assert got == exp
+
+
+def test_shard_rejects_open_gop_cross_reference():
+    import sys
+    sys.path[:0] = [REPO]
+    from tiny_mp2v_dec_amd.records import Parsed, generate_es
+    from tiny_mp2v_dec_amd.shard import shard_batch
+    es = generate_es(width=176, height=144, chroma_format=1, n_gops=2, gop_n=6, gop_m=3, seed=5)
+    p = Parsed(es, 176, 144, 1)
+    # make picture 7's forward reference point into GOP 0 and mark an MB as using it
+    p.gop[:] = np.arange(p.npics) // 6
+    d = 7
+    if p.pics[d]["picture_coding_type"] == 1:
+        d = 8
+    p.pics[d]["fwd_slot"] = 0
+    first = int(p.pics[d]["mb_first"])
+    p.mbs["flags"][first] = 2
+    with pytest.raises(ValueError):
+        shard_batch(p, 1, 2)

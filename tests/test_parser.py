@@ -1,0 +1,148 @@
+"""CPU: host record emitter (ES -> records) — record invariants, display order, and the
+reference input contract: out-of-contract streams are rejected cleanly instead of
+reproducing the reference's undefined behaviour."""
+import numpy as np
+import pytest
+
+from conftest import load_manifest, read_stream
+from tiny_mp2v_dec_amd import _lib
+from tiny_mp2v_dec_amd.records import Parsed, generate_es
+
+MANIFEST = {e["name"]: e for e in load_manifest()}
+
+
+def _parse(es, w=176, h=144, cf=1, **kw):
+    return Parsed(es, w, h, cf, **kw)
+
+
+def _start_codes(es, code):
+    out = []
+    i = es.find(b"\x00\x00\x01" + bytes([code]))
+    while i >= 0:
+        out.append(i)
+        i = es.find(b"\x00\x00\x01" + bytes([code]), i + 1)
+    return out
+
+
+def _set_bit(es, byte_off, bit, value):
+    b = bytearray(es)
+    pos = byte_off * 8 + bit
+    mask = 0x80 >> (pos % 8)
+    if value:
+        b[pos // 8] |= mask
+    else:
+        b[pos // 8] &= ~mask & 0xFF
+    return bytes(b)
+
+
+def _pcext_offsets(es):
+    """byte offsets of picture_coding_extension payloads (after the 4-byte start code)"""
+    return [o + 4 for o in _start_codes(es, 0xB5) if (es[o + 4] >> 4) == 8]
+
+
+def test_record_invariants_on_golden_stream():
+    e = MANIFEST["ipb420_field"]
+    p = _parse(read_stream(e))
+    nmb = 11 * 9
+    assert len(p.mbs) == p.npics * nmb
+    for d in range(p.npics):
+        m = p.mbs[d * nmb:(d + 1) * nmb]
+        assert np.array_equal(m["x"], np.arange(nmb) % 11)
+        assert np.array_equal(m["y"], np.arange(nmb) // 11)
+        # coefficient words of a picture are one contiguous, ordered range
+        assert np.array_equal(m["coef_off"][1:], m["coef_off"][:-1] + m["ncoef"][:-1])
+    blocks = (p.coefs >> 22) & 15
+    assert blocks.max() < 6
+    intra = (p.mbs["flags"] & _lib.MB_INTRA) != 0
+    assert np.all(p.mbs["cbp"][intra] == 0x3F)
+    # every field-MC MB carries two vectors; DCT_FIELD only on coded MBs
+    dctf = (p.mbs["flags"] & _lib.MB_DCT_FIELD) != 0
+    assert np.all(p.mbs["cbp"][dctf] != 0)
+    assert np.any((p.mbs["flags"] & _lib.MB_FIELD_MC) != 0)
+
+
+def test_display_order_matches_reference_scheduler():
+    """B pictures out at once, I/P delayed by one anchor (reference decoder.cpp:346-369)."""
+    e = MANIFEST["ipb420_qcif"]
+    p = _parse(read_stream(e))
+    pct = p.pics["picture_coding_type"]
+    # coding order per closed GOP with leading B: I B B P B B P B B P B B
+    assert list(pct[:12]) == [1, 3, 3, 2, 3, 3, 2, 3, 3, 2, 3, 3]
+    assert list(p.display[:6]) == [1, 2, 0, 4, 5, 3]
+    assert sorted(p.display) == list(range(p.npics))
+    assert list(p.gop) == [0] * 12 + [1] * 12
+    p2 = _parse(read_stream(e), reordering=False)
+    assert list(p2.display) == list(range(p2.npics))
+
+
+def test_threads_do_not_change_records():
+    es = read_stream(MANIFEST["stress_mv_fcode4"])
+    a = Parsed(es, 352, 288, 2, threads=1)
+    b = Parsed(es, 352, 288, 2, threads=8)
+    assert np.array_equal(a.mbs, b.mbs) and np.array_equal(a.coefs, b.coefs) and np.array_equal(a.pics, b.pics)
+
+
+def _expect(status, fn):
+    with pytest.raises(_lib.Mp2vgError) as ei:
+        fn()
+    assert ei.value.status == status, str(ei.value)
+
+
+def test_reject_missing_quant_matrix_extension():
+    """reference dereferences m_quant_matrix_extension unconditionally (decoder.cpp:187-190)"""
+    es = generate_es(width=176, height=144, n_gops=1, gop_n=4, gop_m=1, leading_b=0)
+    b = bytearray()
+    offs = _start_codes(es, 0xB5)
+    qme = [o for o in offs if (es[o + 4] >> 4) == 3]
+    last = 0
+    for o in qme:
+        b += es[last:o]
+        nxt = es.find(b"\x00\x00\x01", o + 4)
+        last = nxt
+    b += es[last:]
+    _expect(-2, lambda: _parse(bytes(b)))
+
+
+def test_reject_field_pictures():
+    es = generate_es(width=176, height=144, n_gops=1, gop_n=4, gop_m=1, leading_b=0)
+    for o in _pcext_offsets(es):  # picture_structure: bits 22-23 of the payload -> '01'
+        es = _set_bit(es, o, 22, 0)
+        es = _set_bit(es, o, 23, 1)
+    _expect(-2, lambda: _parse(es))
+
+
+def test_reject_intra_vlc_format_zero():
+    """reference applies the non-intra '1s' rule to intra blocks (mb_decoder.cpp:79-88)"""
+    es = generate_es(width=176, height=144, n_gops=1, gop_n=2, gop_m=1, leading_b=0, mix=1)
+    for o in _pcext_offsets(es):  # intra_vlc_format: bit 28
+        es = _set_bit(es, o, 28, 0)
+    _expect(-2, lambda: _parse(es))
+
+
+def test_reject_chroma_format_mismatch():
+    es = generate_es(width=176, height=144, chroma_format=1, n_gops=1, gop_n=2, gop_m=1, leading_b=0)
+    _expect(-2, lambda: _parse(es, cf=2))
+
+
+def test_reject_truncated_stream():
+    es = generate_es(width=176, height=144, n_gops=1, gop_n=3, gop_m=1, leading_b=0)
+    cut = _start_codes(es, 0x05)[-1]  # drop everything from the last picture's 5th slice on
+    with pytest.raises(_lib.Mp2vgError):
+        _parse(es[:cut])
+
+
+def test_reject_bad_geometry():
+    es = generate_es(width=176, height=144, n_gops=1, gop_n=2, gop_m=1, leading_b=0)
+    _expect(-1, lambda: Parsed(es, 170, 144, 1))
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_generated_streams_parse(seed):
+    """The writer only emits the accepted subset: every random configuration parses."""
+    rng = np.random.default_rng(seed)
+    cf = int(rng.integers(1, 4))
+    es = generate_es(width=176, height=144, chroma_format=cf, n_gops=2, gop_n=int(rng.integers(1, 13)),
+                     gop_m=int(rng.integers(1, 4)), seed=seed, frame_pred_frame_dct=int(rng.integers(0, 2)),
+                     f_code=int(rng.integers(1, 6)), big_level_permille=100, escape_permille=200)
+    p = _parse(es, cf=cf)
+    assert p.npics >= 2

@@ -15,6 +15,7 @@ REPO = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 OUT = os.path.join(PKG, "_build")
 LIB = os.path.join(OUT, "libmp2vg.so")
+CLI = os.path.join(OUT, "tiny_mp2v_dec_gpu")
 ARCH = os.environ.get("MP2VG_OFFLOAD_ARCH", "gfx950")
 
 
@@ -73,6 +74,14 @@ def build(verbose=False):
             raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
         if verbose:
             print("linked", os.path.relpath(LIB, REPO))
+    # the reference CLI sample rebuilt against the drop-in header (include/mp2v_decoder.h)
+    cli_src = os.path.join(REPO, "tools", "tiny_mp2v_dec_gpu.cpp")
+    if os.path.exists(cli_src) and _stale(CLI, [cli_src, LIB] + hdrs):
+        cmd = ["g++", "-std=c++17", "-O2", "-I", os.path.join(REPO, "include"), cli_src, "-o", CLI, "-L", OUT,
+               "-lmp2vg", "-Wl,-rpath,$ORIGIN"]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"cli build failed: {' '.join(cmd)}\n{r.stderr}")
     return LIB
 
 
