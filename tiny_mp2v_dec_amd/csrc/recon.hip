@@ -1,5 +1,17 @@
-// recon.hip — HIP kernels of the macroblock reconstruct path (see recon_kernel.h for the map to
-// the reference).  Written for gfx950 only: wave64, LDS per wave, no CUDA-compat layer.
+// recon.hip — HIP kernels of the macroblock reconstruct path (gfx950 / CDNA4 only: wave64,
+// packed 16-bit VALU, v_lerp_u8, LDS per wave; no CUDA-compat layer).  See recon_kernel.h for
+// the map to the reference.
+//
+// Work decomposition: one workgroup (4 waves) per slice (= MB row, XCD-aware order); each wave
+// reconstructs groups of G = 4 consecutive macroblocks with wave-private LDS:
+//   A  group records (scalar loads) + first 64 coefficient words
+//   B  reference-row loads for every pixel row of the group (one lane per row: 16-px luma rows,
+//      8/16-px chroma rows), issued before the transform so their latency hides behind it
+//   C  dequant: lanes = coefficient words -> coded-block slots (compacted) in LDS
+//   D  SSE2-exact IDCT on packed i16 pairs (two lines per lane, v_pk_add_i16 clamp =
+//      _mm_adds_epi16), mismatch control folded into pass 1 (ds_swizzle parity reduce)
+//   E  prediction (cascaded half-pel with v_lerp_u8 == _mm_avg_epu8, bidir average) + residual
+//      with clamp (packed i16) and one 16-B / 8-B store per row
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -8,53 +20,72 @@
 
 namespace mp2vg {
 
-// ------------------------------------------------------------------------------------------
-// 16-bit saturating helpers (SSE2 semantics: _mm_adds/_mm_subs_epi16 saturate, _mm_slli_epi16
-// wraps, _mm_mulhi_epi16 = (a*b)>>16).
-__device__ __forceinline__ short adds16(short a, short b) { return __builtin_elementwise_add_sat(a, b); }
-__device__ __forceinline__ short subs16(short a, short b) { return __builtin_elementwise_sub_sat(a, b); }
-__device__ __forceinline__ short mulhi16(short a, int c) { return (short)(((int)a * c) >> 16); }
-__device__ __forceinline__ short shl16(short a, int n) { return (short)((unsigned short)a << n); }
+typedef short short2_t __attribute__((ext_vector_type(2)));
 
-// idct_sse2.hpp:23-65 for one lane
-__device__ __forceinline__ void idct_1d(short s[8]) {
-    const short v15 = adds16(shl16(mulhi16(s[0], 27145), 1), shl16(s[0], 1));
-    const short v26 = adds16(mulhi16(s[1], -5037), shl16(s[1], 2));
-    const short v21 = adds16(mulhi16(s[2], -19954), shl16(s[2], 2));
-    const short v28 = adds16(shl16(mulhi16(s[3], -22089), 1), shl16(s[3], 2));
-    const short v16 = adds16(shl16(mulhi16(s[4], 27145), 1), shl16(s[4], 1));
-    const short v25 = adds16(mulhi16(s[5], 14567), shl16(s[5], 1));
-    const short v22 = adds16(shl16(mulhi16(s[6], 17391), 1), s[6]);
-    const short v27 = shl16(mulhi16(s[7], 25570), 1);
-    const short v19 = subs16(v25, v28);
-    const short v20 = subs16(v26, v27);
-    const short v23 = adds16(v26, v27);
-    const short v24 = adds16(v25, v28);
-    const short v7 = adds16(v23, v24);
-    const short v11 = adds16(v21, v22);
-    const short v13 = subs16(v23, v24);
-    const short v17 = subs16(v21, v22);
-    const short v8 = adds16(v15, v16);
-    const short v9 = subs16(v15, v16);
-    const short v18 = mulhi16(subs16(v19, v20), 25079);
-    const short v12 = subs16(v18, adds16(v19, mulhi16(v19, 20090)));
-    const short v14 = subs16(subs16(v20, mulhi16(v20, 30068)), v18);
-    const short v6 = subs16(shl16(v14, 1), v7);
-    const short v5 = subs16(adds16(v13, mulhi16(v13, 27145)), v6);
-    const short v4 = adds16(v5, shl16(v12, 1));
-    const short v10 = subs16(adds16(v17, mulhi16(v17, 27145)), v11);
-    const short v0 = adds16(v8, v11);
-    const short v1 = adds16(v9, v10);
-    const short v2 = subs16(v9, v10);
-    const short v3 = subs16(v8, v11);
-    s[0] = adds16(v0, v7);
-    s[1] = adds16(v1, v6);
-    s[2] = adds16(v2, v5);
-    s[3] = subs16(v3, v4);
-    s[4] = adds16(v3, v4);
-    s[5] = subs16(v2, v5);
-    s[6] = subs16(v1, v6);
-    s[7] = subs16(v0, v7);
+// ------------------------------------------------------------------------------------------
+// SSE2 16-bit semantics on packed pairs (two independent IDCT lines per lane):
+//   _mm_adds/_mm_subs_epi16 saturate, _mm_slli_epi16 wraps, _mm_mulhi_epi16 = (a*b)>>16
+__device__ __forceinline__ short2_t adds2(short2_t a, short2_t b) { return __builtin_elementwise_add_sat(a, b); }
+__device__ __forceinline__ short2_t subs2(short2_t a, short2_t b) { return __builtin_elementwise_sub_sat(a, b); }
+__device__ __forceinline__ short2_t shl2(short2_t a, int n) {
+    return __builtin_bit_cast(short2_t, __builtin_bit_cast(ushort2, a) << (unsigned short)n);
+}
+__device__ __forceinline__ short2_t mulhi2(short2_t a, int c) {
+    short2_t r;
+    r.x = (short)(((int)a.x * c) >> 16);
+    r.y = (short)(((int)a.y * c) >> 16);
+    return r;
+}
+
+// idct_sse2.hpp:23-65, two lanes of the SSE2 vector at once
+__device__ __forceinline__ void idct_1d(short2_t s[8]) {
+    const short2_t v15 = adds2(shl2(mulhi2(s[0], 27145), 1), shl2(s[0], 1));
+    const short2_t v26 = adds2(mulhi2(s[1], -5037), shl2(s[1], 2));
+    const short2_t v21 = adds2(mulhi2(s[2], -19954), shl2(s[2], 2));
+    const short2_t v28 = adds2(shl2(mulhi2(s[3], -22089), 1), shl2(s[3], 2));
+    const short2_t v16 = adds2(shl2(mulhi2(s[4], 27145), 1), shl2(s[4], 1));
+    const short2_t v25 = adds2(mulhi2(s[5], 14567), shl2(s[5], 1));
+    const short2_t v22 = adds2(shl2(mulhi2(s[6], 17391), 1), s[6]);
+    const short2_t v27 = shl2(mulhi2(s[7], 25570), 1);
+    const short2_t v19 = subs2(v25, v28);
+    const short2_t v20 = subs2(v26, v27);
+    const short2_t v23 = adds2(v26, v27);
+    const short2_t v24 = adds2(v25, v28);
+    const short2_t v7 = adds2(v23, v24);
+    const short2_t v11 = adds2(v21, v22);
+    const short2_t v13 = subs2(v23, v24);
+    const short2_t v17 = subs2(v21, v22);
+    const short2_t v8 = adds2(v15, v16);
+    const short2_t v9 = subs2(v15, v16);
+    const short2_t v18 = mulhi2(subs2(v19, v20), 25079);              // op4
+    const short2_t v12 = subs2(v18, adds2(v19, mulhi2(v19, 20090)));  // op3
+    const short2_t v14 = subs2(subs2(v20, mulhi2(v20, 30068)), v18);  // op1
+    const short2_t v6 = subs2(shl2(v14, 1), v7);
+    const short2_t v5 = subs2(adds2(v13, mulhi2(v13, 27145)), v6);    // op0
+    const short2_t v4 = adds2(v5, shl2(v12, 1));
+    const short2_t v10 = subs2(adds2(v17, mulhi2(v17, 27145)), v11);  // op0
+    const short2_t v0 = adds2(v8, v11);
+    const short2_t v1 = adds2(v9, v10);
+    const short2_t v2 = subs2(v9, v10);
+    const short2_t v3 = subs2(v8, v11);
+    s[0] = adds2(v0, v7);
+    s[1] = adds2(v1, v6);
+    s[2] = adds2(v2, v5);
+    s[3] = subs2(v3, v4);
+    s[4] = adds2(v3, v4);
+    s[5] = subs2(v2, v5);
+    s[6] = subs2(v1, v6);
+    s[7] = subs2(v0, v7);
+}
+
+// two 8 x int16 lines (16 B each) -> 8 packed pairs (a[u], b[u])
+__device__ __forceinline__ void interleave(const uint4& a, const uint4& b, short2_t s[8]) {
+    const uint32_t av[4] = {a.x, a.y, a.z, a.w}, bv[4] = {b.x, b.y, b.z, b.w};
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        s[2 * i] = __builtin_bit_cast(short2_t, __builtin_amdgcn_perm(bv[i], av[i], 0x05040100u));
+        s[2 * i + 1] = __builtin_bit_cast(short2_t, __builtin_amdgcn_perm(bv[i], av[i], 0x07060302u));
+    }
 }
 
 // scan position -> raster (v*8+u), zig-zag / alternate (reference scan_c.cpp:41-57)
@@ -73,40 +104,15 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// SWAR per-byte rounding-up average: (a + b + 1) >> 1 on 4 packed u8 (== _mm_avg_epu8)
-__device__ __forceinline__ uint32_t avg4(uint32_t a, uint32_t b) {
-    return (a | b) - (((a ^ b) >> 1) & 0x7f7f7f7fu);
-}
-
-// 5 consecutive bytes at p (any alignment) -> {bytes 0..3, bytes 1..4}
-__device__ __forceinline__ void load5(const uint8_t* p, uint32_t& lo, uint32_t& sh1) {
-    uintptr_t a = (uintptr_t)p;
-    const uint32_t* w = (const uint32_t*)(a & ~(uintptr_t)3);
-    uint32_t s = (uint32_t)(a & 3) * 8;
-    uint64_t v = ((uint64_t)w[1] << 32) | w[0];
-    v >>= s;
-    lo = (uint32_t)v;
-    sh1 = (uint32_t)(v >> 8);
-}
+// per-byte (a + b + 1) >> 1 on 4 packed u8 == _mm_avg_epu8: one v_lerp_u8 (rounding bit per byte)
+__device__ __forceinline__ uint32_t avg4(uint32_t a, uint32_t b) { return __builtin_amdgcn_lerp(a, b, 0x01010101u); }
 
 template <int CF>
 struct Fmt {
     static constexpr int NB = CF == 1 ? 6 : (CF == 2 ? 8 : 12);  // blocks per MB
     static constexpr int CW = CF == 3 ? 16 : 8;                  // chroma MB width
     static constexpr int CH = CF == 1 ? 8 : 16;                  // chroma MB height
-    static constexpr int ITEMS = 64 + 2 * (CW / 4) * CH;         // 4-pixel items per MB
 };
-
-// which coded block covers MB-plane pixel row py / column px (mb_decoder.cpp:176-195)
-template <int CF>
-__device__ __forceinline__ int block_of(int plane, int px, int py, bool dctf) {
-    if (plane == 0) return (dctf ? (py & 1) : (py >> 3)) * 2 + (px >> 3);
-    int base = plane == 1 ? 4 : 5;
-    if (CF == 1) return base;
-    bool lower = (dctf ? (py & 1) : (py >> 3)) != 0;
-    int k = (px >= 8 ? 2 : 0) + (lower ? 1 : 0);
-    return base + 2 * k;
-}
 
 // origin of block b in its MB plane image and its row step (mb_decoder.cpp:176-195)
 template <int CF>
@@ -124,9 +130,9 @@ __device__ __forceinline__ void block_origin(int b, bool dctf, int& plane, int& 
         return;
     }
     plane = (b & 1) ? 2 : 1;
-    int k = (b - 4) >> 1;
+    const int k = (b - 4) >> 1;
     x0 = k >= 2 ? 8 : 0;
-    bool lower = (k & 1);
+    const bool lower = (k & 1);
     if (dctf && CF != 1) {
         y0 = lower ? 1 : 0;
         ys = 2;
@@ -135,61 +141,89 @@ __device__ __forceinline__ void block_origin(int b, bool dctf, int& plane, int& 
     }
 }
 
-constexpr int WAVES = 4;
+// the block covering the left (x<8) half of MB-plane row py; the right half is +1 (luma) or
+// +4 (4:4:4 chroma: blocks 4/8, 6/10, 5/9, 7/11)
+template <int CF>
+__device__ __forceinline__ int left_block(int plane, int py, bool dctf) {
+    const int lower = dctf ? (py & 1) : (py >> 3);
+    if (plane == 0) return lower * 2;
+    const int base = plane == 1 ? 4 : 5;
+    if (CF == 1) return base;
+    return base + 2 * lower;
+}
 
-// Residual image of one MB in LDS: luma 16x16, then Cb CW x CH, then Cr (int16)
+constexpr int WAVES = 4;
+constexpr int G = 4;  // macroblocks per wave group
+
+// Residual image of one MB in LDS (int16): luma 16x16, then Cb CW x CH, then Cr.  Inside each
+// group of 4 pixels the order is x0, x0+2, x0+1, x0+3: one v_perm unpacks the matching
+// prediction bytes into (x0, x0+2) / (x0+1, x0+3) pairs for packed i16 math, and IDCT pass 2
+// (columns x, x+2 per lane) stores one dword per output row.
 template <int CF>
 struct ResLayout {
     using F = Fmt<CF>;
     static constexpr int SIZE = 256 + 2 * F::CW * F::CH;
     __device__ static constexpr int base(int plane) { return plane == 0 ? 0 : 256 + (plane - 1) * F::CW * F::CH; }
     __device__ static constexpr int width(int plane) { return plane == 0 ? 16 : F::CW; }
+    __device__ static int pos(int x) { return (x & ~3) | ((x & 1) << 1) | ((x >> 1) & 1); }
 };
 
-// item index (G MBs side by side) -> MB k, plane, pixel column px (multiple of 4), row py.
-// Items of one pixel row of the group are consecutive so a row of lanes stores 16*G contiguous
-// bytes of luma (4*CW*G/4 of chroma).
-template <int CF, int G>
-__device__ __forceinline__ void item_coords(int it, int& k, int& plane, int& px, int& py) {
-    using F = Fmt<CF>;
-    constexpr int LUMA = G * 64;
-    constexpr int CPR = F::CW / 4;       // chroma items per MB row
-    constexpr int CPL = G * CPR * F::CH;  // chroma items per plane
-    if (it < LUMA) {
+// select one of three wave-uniform per-plane values by a lane-varying plane index (plain
+// indexing makes the compiler re-load the kernel-argument array with per-lane vector loads)
+template <class T>
+__device__ __forceinline__ T gsel(const T (&v)[3], int plane) {
+    return plane == 0 ? v[0] : (plane == 1 ? v[1] : v[2]);
+}
+
+// Per-MB wave-uniform state of a group (SGPRs).  Fields are 4-vectors with named components:
+// with plain arrays the compiler lowers the per-lane pick() below into a lane-indexed SCRATCH
+// load of a stack copy of the group.
+typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+struct Group {
+    u4v mbx, mby, flags, cbp, qs, mv[4];  // mv[r*2+s], component k = MB
+    u4v slot_base, coef_rel;
+    int nslots, ncoef;
+    uint32_t coef0;
+};
+
+// select component k (lane-varying) of a wave-uniform 4-vector: three v_cndmask
+__device__ __forceinline__ uint32_t pick(const u4v& v, int k) {
+    return k == 0 ? v.x : (k == 1 ? v.y : (k == 2 ? v.z : v.w));
+}
+
+// Pixel-row passes of a group: pass 0 = the 64 luma rows (4 MBs x 16); 4:2:0 pass 1 = Cb + Cr
+// (4 x 8 each); 4:2:2 / 4:4:4 pass 1 = Cb, pass 2 = Cr (4 x 16 each).  Rows of the same pixel
+// row of adjacent MBs sit in adjacent lanes.
+template <int CF>
+struct Passes {
+    static constexpr int N = CF == 1 ? 2 : 3;
+};
+template <int CF, int J>
+__device__ __forceinline__ void pass_row(int lane, int& k, int& plane, int& py) {
+    k = lane & 3;
+    py = lane >> 2;
+    if (J == 0) {
         plane = 0;
-        py = it / (4 * G);
-        const int rem = it % (4 * G);
-        k = rem >> 2;
-        px = (rem & 3) * 4;
+    } else if (CF == 1) {
+        plane = 1 + (lane >> 5);
+        py = (lane & 31) >> 2;
     } else {
-        int c = it - LUMA;
-        plane = c < CPL ? 1 : 2;
-        c = c < CPL ? c : c - CPL;
-        py = c / (G * CPR);
-        const int rem = c % (G * CPR);
-        k = rem / CPR;
-        px = (rem % CPR) * 4;
+        plane = J;
     }
 }
 
-// select the k-th of G wave-uniform values (k lane-varying, G <= 4)
-template <int G, class T>
-__device__ __forceinline__ T pick(const T (&v)[G], int k) {
-    T r = v[0];
-#pragma unroll
-    for (int i = 1; i < G; i++) r = (k == i) ? v[i] : r;
-    return r;
-}
-
-// Raw reference words for one 4-pixel item in one direction: rows Y and Y+step, two aligned
-// dwords each (the second row only when the vector is vertically half-pel).
-struct Tap {
-    uint32_t w0, w1, w2, w3;
+// one prediction direction of one pixel row: raw dwords from the dword-aligned reference x
+template <int NW>  // output dwords: 4 (16-px row) or 2 (8-px row)
+struct RowTap {
+    static constexpr int ND = NW + 1;  // dwords loaded per reference row
+    uint32_t a[ND], b[ND];             // rows Y and Y + step
+    int sh, hxy;
 };
 
-template <int CF>
-__device__ __forceinline__ void tap_geometry(uint32_t mvw, int plane, int gx, int py, int mby_base, bool field,
-                                             int fs, int stride, int ph, int& off0, int& off1, int& sh, int& hxy) {
+template <int CF, int NW>
+__device__ __forceinline__ void row_tap_issue(RowTap<NW>& t, const uint8_t* __restrict__ plane_base, uint32_t mvw,
+                                              int plane, int gx, int py, int mby_base, bool field, int fs, int stride,
+                                              int ph) {
     int mvx = (short)(mvw & 0xffff), mvy = (short)(mvw >> 16);
     if (plane > 0) {  // apply_chroma_scale (mb_decoder.cpp:198-206): arithmetic shift
         if (CF < 3) mvx >>= 1;
@@ -200,56 +234,159 @@ __device__ __forceinline__ void tap_geometry(uint32_t mvw, int plane, int gx, in
     if (!field) {
         Y = mby_base + py + (mvy >> 1);
         step = 1;
-    } else {  // field MC (mb_decoder.cpp:229-236): row 2q + field_select, vector r = py & 1
+    } else {  // field MC (mb_decoder.cpp:229-236): rows 2q + field_select, vector r = py & 1
         Y = mby_base + fs + 2 * ((py >> 1) + (mvy >> 1));
         step = 2;
     }
-    // clamp into the plane: out-of-contract vectors can never fault (inactive in contract)
+    // clamp into the plane so out-of-contract vectors can never fault (inactive in contract)
     const int Xc = min(max(X, 0), stride - 4);
     const int Y0 = min(max(Y, 0), ph - 1);
     const int Y1 = min(max(Y + step, 0), ph - 1);
-    off0 = Y0 * stride + (Xc & ~3);
-    off1 = Y1 * stride + (Xc & ~3);
-    sh = (Xc & 3) * 8;
-    hxy = (mvx & 1) | ((mvy & 1) << 1);
-}
-
-__device__ __forceinline__ Tap issue_tap(const uint8_t* __restrict__ plane_base, int off0, int off1, int hxy) {
-    Tap t;
-    const uint32_t* r0 = (const uint32_t*)(plane_base + off0);
-    t.w0 = r0[0];
-    t.w1 = r0[1];
-    if (hxy & 2) {
-        const uint32_t* r1 = (const uint32_t*)(plane_base + off1);
-        t.w2 = r1[0];
-        t.w3 = r1[1];
+    t.sh = Xc & 3;
+    t.hxy = (mvx & 1) | ((mvy & 1) << 1);
+    const uint32_t* r0 = (const uint32_t*)(plane_base + (size_t)Y0 * stride + (Xc & ~3));
+#pragma unroll
+    for (int i = 0; i < RowTap<NW>::ND; i++) t.a[i] = r0[i];
+    if (t.hxy & 2) {
+        const uint32_t* r1 = (const uint32_t*)(plane_base + (size_t)Y1 * stride + (Xc & ~3));
+#pragma unroll
+        for (int i = 0; i < RowTap<NW>::ND; i++) t.b[i] = r1[i];
     } else {
-        t.w2 = t.w3 = 0;
+#pragma unroll
+        for (int i = 0; i < RowTap<NW>::ND; i++) t.b[i] = t.a[i];
     }
-    return t;
 }
 
-// cascaded half-pel average (mc_sse2.hpp:5-39 == mc_c.hpp:15)
-__device__ __forceinline__ uint32_t finish_tap(const Tap& t, int sh, int hxy) {
-    const uint64_t v0 = (((uint64_t)t.w1 << 32) | t.w0) >> sh;
-    const uint32_t A = (uint32_t)v0, B = (uint32_t)(v0 >> 8);
-    if (!(hxy & 2)) return (hxy & 1) ? avg4(A, B) : A;
-    const uint64_t v1 = (((uint64_t)t.w3 << 32) | t.w2) >> sh;
-    const uint32_t C = (uint32_t)v1, D = (uint32_t)(v1 >> 8);
-    return (hxy & 1) ? avg4(avg4(A, B), avg4(C, D)) : avg4(A, C);
+// cascaded half-pel average of one row (mc_sse2.hpp:5-39 == mc_c.hpp:15), branch-free:
+// avg(x, x) == x, so the unused taps are replaced by the used ones.
+template <int NW>
+__device__ __forceinline__ void row_tap_finish(const RowTap<NW>& t, uint32_t (&p)[4]) {
+    const uint32_t s = (uint32_t)t.sh;
+    const bool hx = t.hxy & 1;
+    uint32_t A[NW + 1], C[NW + 1];
+#pragma unroll
+    for (int d = 0; d < NW; d++) {
+        A[d] = __builtin_amdgcn_alignbyte(t.a[d + 1], t.a[d], s);
+        C[d] = __builtin_amdgcn_alignbyte(t.b[d + 1], t.b[d], s);
+    }
+    A[NW] = t.a[NW] >> (8 * s);  // only its byte 0 is used (the 17th / 9th pixel)
+    C[NW] = t.b[NW] >> (8 * s);
+#pragma unroll
+    for (int d = 0; d < NW; d++) {
+        const uint32_t B = __builtin_amdgcn_alignbyte(A[d + 1], A[d], 1u);
+        const uint32_t D = __builtin_amdgcn_alignbyte(C[d + 1], C[d], 1u);
+        const uint32_t r0 = avg4(A[d], hx ? B : A[d]);
+        const uint32_t r1 = avg4(C[d], hx ? D : C[d]);
+        p[d] = avg4(r0, r1);  // r1 == r0 when the vector is vertically full-pel
+    }
 }
 
-// Per-MB wave-uniform state of the group
-template <int G>
-struct Group {
-    uint32_t mbx[G], mby[G], flags[G], cbp[G], qs[G], mv[4][G];  // mv[r*2+s][k]
-    int slot_base[G];
-    int coef_rel[G];  // first coefficient word of MB k, relative to the group's first
-    int nslots, ncoef;
-    uint32_t coef0;
+template <int CF, int ABL>
+struct Kern {
+    using F = Fmt<CF>;
+    using RL = ResLayout<CF>;
+    static constexpr int NB = F::NB;
+    static constexpr int MAXS = G * NB;  // coded-block slots per group
+    static constexpr int NWC = F::CW / 4;  // dwords per chroma row
 };
 
-template <int CF, int G, int ABL = 0>
+template <int CF, int J, int NW>
+__device__ __forceinline__ void issue_pass(const Group& S, int lane, const Geo& geo, const uint8_t* ref_fwd,
+                                           const uint8_t* ref_bwd, RowTap<NW>& tf, RowTap<NW>& tb, bool skip) {
+    using F = Fmt<CF>;
+    int k, plane, py;
+    pass_row<CF, J>(lane, k, plane, py);
+    const uint32_t fl = pick(S.flags, k);
+    const bool none = (fl & MP2VG_MB_INTRA) || skip;
+    const bool bwd = fl & MP2VG_MB_BWD;
+    const bool fwd = !none && ((fl & MP2VG_MB_FWD) || !bwd);
+    const bool field = fl & MP2VG_MB_FIELD_MC;
+    const int pw = plane == 0 ? 16 : F::CW;
+    const int phm = plane == 0 ? 16 : F::CH;
+    const int gx = (int)pick(S.mbx, k) * pw;
+    const int mbyb = (int)pick(S.mby, k) * phm;
+    const int r = field ? (py & 1) : 0;
+    const int stride = gsel(geo.stride, plane);
+    const int ph = gsel(geo.ph, plane);
+    tf.hxy = tb.hxy = 0;
+    tf.sh = tb.sh = 0;
+    if (fwd) {
+        const uint32_t mvw = r ? pick(S.mv[2], k) : pick(S.mv[0], k);
+        row_tap_issue<CF, NW>(tf, ref_fwd + gsel(geo.plane_off, plane), mvw, plane, gx, py, mbyb, field,
+                              (fl >> (8 + 2 * r)) & 1, stride, ph);
+    }
+    if (!none && bwd) {
+        const uint32_t mvw = r ? pick(S.mv[3], k) : pick(S.mv[1], k);
+        row_tap_issue<CF, NW>(tb, ref_bwd + gsel(geo.plane_off, plane), mvw, plane, gx, py, mbyb, field,
+                              (fl >> (9 + 2 * r)) & 1, stride, ph);
+    }
+}
+
+template <int CF, int J, int NW, int ABL>
+__device__ __forceinline__ void finish_pass(const Group& S, int ng, int lane, const Geo& geo, uint8_t* dst_slot,
+                                            const short* s_res_wave, const RowTap<NW>& tf, const RowTap<NW>& tb) {
+    using F = Fmt<CF>;
+    using RL = ResLayout<CF>;
+    int k, plane, py;
+    pass_row<CF, J>(lane, k, plane, py);
+    if (k >= ng) return;
+    const uint32_t fl = pick(S.flags, k);
+    const bool intra = fl & MP2VG_MB_INTRA;
+    const bool bwd = fl & MP2VG_MB_BWD;
+    const bool fwd = !intra && ((fl & MP2VG_MB_FWD) || !bwd);
+    uint32_t p[4] = {0, 0, 0, 0};
+    if (!intra) {
+        uint32_t pf[4] = {0, 0, 0, 0}, pb[4] = {0, 0, 0, 0};
+        if (fwd) row_tap_finish<NW>(tf, pf);
+        if (bwd) row_tap_finish<NW>(tb, pb);
+#pragma unroll
+        for (int d = 0; d < NW; d++) p[d] = (fwd && bwd) ? avg4(pf[d], pb[d]) : (fwd ? pf[d] : pb[d]);  // mc_sse2.hpp:78-84
+    }
+    // put: packus(res); add: packus(adds(pred, res))   (idct_sse2.hpp:106-119)
+    const uint32_t cbpk = pick(S.cbp, k);
+    const int lb = left_block<CF>(plane, py, fl & MP2VG_MB_DCT_FIELD);
+    const int rb = (plane == 0) ? lb + 1 : lb + 4;
+    const bool cl = cbpk & (1u << lb);
+    const bool cr = NW == 4 && (cbpk & (1u << rb));
+    uint32_t out[4] = {p[0], p[1], p[2], p[3]};
+    if (cl || cr) {
+        const short* res = s_res_wave + k * RL::SIZE + RL::base(plane) + py * RL::width(plane);
+        uint32_t rv[8];
+        const uint4 r0 = *(const uint4*)&res[0];
+        rv[0] = r0.x; rv[1] = r0.y; rv[2] = r0.z; rv[3] = r0.w;
+        if (NW == 4) {
+            const uint4 r1 = *(const uint4*)&res[8];
+            rv[4] = r1.x; rv[5] = r1.y; rv[6] = r1.z; rv[7] = r1.w;
+        }
+#pragma unroll
+        for (int d = 0; d < NW; d++) {
+            if (!(d < 2 ? cl : cr)) continue;
+            // pairs (x0, x0+2) and (x0+1, x0+3) as packed i16
+            const uint32_t lo = __builtin_amdgcn_perm(0u, p[d], 0x0c020c00u);
+            const uint32_t hi = __builtin_amdgcn_perm(0u, p[d], 0x0c030c01u);
+            short2_t a = __builtin_bit_cast(short2_t, lo) + __builtin_bit_cast(short2_t, rv[2 * d]);
+            short2_t c = __builtin_bit_cast(short2_t, hi) + __builtin_bit_cast(short2_t, rv[2 * d + 1]);
+            const short2_t z = {0, 0}, m = {255, 255};
+            a = __builtin_elementwise_min(__builtin_elementwise_max(a, z), m);
+            c = __builtin_elementwise_min(__builtin_elementwise_max(c, z), m);
+            // bytes: x0 = a.lo, x0+1 = c.lo, x0+2 = a.hi, x0+3 = c.hi
+            out[d] = __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, c), __builtin_bit_cast(uint32_t, a), 0x06020400u);
+        }
+    }
+    const int pw = plane == 0 ? 16 : F::CW;
+    const int phm = plane == 0 ? 16 : F::CH;
+    uint8_t* dst = dst_slot + gsel(geo.plane_off, plane) +
+                   (size_t)((int)pick(S.mby, k) * phm + py) * gsel(geo.stride, plane) + (int)pick(S.mbx, k) * pw;
+    if (ABL & 8) {
+        asm volatile("" ::"v"(out[0]), "v"(out[1]), "v"(out[2]), "v"(out[3]));
+    } else if (NW == 4) {
+        *(uint4*)dst = make_uint4(out[0], out[1], out[2], out[3]);
+    } else {
+        *(uint2*)dst = make_uint2(out[0], out[1]);
+    }
+}
+
+template <int CF, int ABL = 0>
 __global__ __launch_bounds__(256) void recon_kernel(const mp2vg_picture_t* __restrict__ pics,
                                                     const uint32_t* __restrict__ mbrec,
                                                     const uint32_t* __restrict__ coefs,
@@ -259,12 +396,10 @@ __global__ __launch_bounds__(256) void recon_kernel(const mp2vg_picture_t* __res
     using F = Fmt<CF>;
     using RL = ResLayout<CF>;
     constexpr int NB = F::NB;
-    constexpr int MAXS = G * NB;                     // coded-block slots per group
-    constexpr int NIT = G * F::ITEMS;                // 4-pixel items per group
-    constexpr int IPL = (NIT + 63) / 64;             // items per lane
+    constexpr int MAXS = G * NB;
+    constexpr int NWC = F::CW / 4;
     __shared__ __attribute__((aligned(16))) short s_blk[WAVES][MAXS][64];  // coef raster -> pass-1 out
-    __shared__ __attribute__((aligned(16))) short s_res[WAVES][G][RL::SIZE];
-    __shared__ int s_par[WAVES][MAXS];
+    __shared__ __attribute__((aligned(16))) short s_res[WAVES][G * RL::SIZE];
     __shared__ uint8_t s_map[WAVES][MAXS];  // slot -> k*16 + b
     __shared__ uint8_t s_W[4][64];
     __shared__ uint8_t s_scan[64];
@@ -272,8 +407,7 @@ __global__ __launch_bounds__(256) void recon_kernel(const mp2vg_picture_t* __res
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    // XCD-aware mapping: consecutive slices (rows of one picture) share an XCD's L2
-    // (bijective: XCD x = b % 8 owns the contiguous range [x*q + min(x, r), ...) of q or q+1 slices)
+    // XCD-aware bijection: XCD x = b % 8 owns the contiguous slice range [x*q + min(x, r), ...)
     const uint32_t b = blockIdx.x, q8 = nslices / 8, r8 = nslices % 8, xcd = b % 8;
     const uint32_t si = xcd * q8 + min(xcd, r8) + b / 8;
     const SliceDesc sd = slices[slice_base + si];
@@ -285,7 +419,6 @@ __global__ __launch_bounds__(256) void recon_kernel(const mp2vg_picture_t* __res
         s_scan[tid] = c_scan_raster[alt][tid];
     }
     for (int i = lane; i < MAXS * 64 / 2; i += 64) ((uint32_t*)s_blk[wave])[i] = 0;
-    for (int i = lane; i < MAXS; i += 64) s_par[wave][i] = 0;
     __syncthreads();
 
     uint8_t* const dst_slot = pool + (uint64_t)pic->dst_slot * geo.slot_bytes;
@@ -294,73 +427,51 @@ __global__ __launch_bounds__(256) void recon_kernel(const mp2vg_picture_t* __res
 
     const uint32_t mb_end = sd.mb_begin + sd.mb_count;
     for (uint32_t g0 = sd.mb_begin + wave * G; g0 < mb_end; g0 += WAVES * G) {
-        // ---- group records (scalar loads; the MB array is padded by G records) ----
+        // ---- A. group records: uniform scalar loads (the MB array is padded by 16 records);
+        //         readfirstlane pins them in SGPRs (else the compiler turns the per-lane pick<>
+        //         selects back into lane-indexed vector loads of the record) ----
         const int ng = min((int)(mb_end - g0), G);
-        Group<G> S;
+        Group S;
         int sb = 0, cr = 0;
         const uint32_t* rp = mbrec + (size_t)g0 * 8;
-        S.coef0 = rp[3];
+#define SLD(i) ((uint32_t)__builtin_amdgcn_readfirstlane((int)rp[i]))
+        S.coef0 = SLD(3);
 #pragma unroll
         for (int k = 0; k < G; k++) {
-            const uint32_t r0 = rp[k * 8 + 0], r1 = rp[k * 8 + 1], r2 = rp[k * 8 + 2];
+            const uint32_t r0 = SLD(k * 8 + 0), r1 = SLD(k * 8 + 1), r2 = SLD(k * 8 + 2);
             const bool live = k < ng;
+            const uint32_t cbpk = live ? ((r1 >> 16) & ((1u << NB) - 1)) : 0u;
             S.mbx[k] = r0 & 0xffff;
             S.mby[k] = r0 >> 16;
             S.flags[k] = live ? (r1 & 0xffff) : (uint32_t)MP2VG_MB_INTRA;
-            S.cbp[k] = live ? ((r1 >> 16) & ((1u << NB) - 1)) : 0u;
+            S.cbp[k] = cbpk;
             S.qs[k] = r2 & 0xff;
-            S.slot_base[k] = sb;
-            S.coef_rel[k] = cr;
-            sb += __builtin_popcount(S.cbp[k]);
+            S.slot_base[k] = (uint32_t)sb;
+            S.coef_rel[k] = (uint32_t)cr;
+            sb += __builtin_popcount(cbpk);
             cr += live ? (int)(r2 >> 16) : 0;
 #pragma unroll
-            for (int q = 0; q < 4; q++) S.mv[q][k] = rp[k * 8 + 4 + q];
+            for (int q = 0; q < 4; q++) S.mv[q][k] = SLD(k * 8 + 4 + q);
         }
+#undef SLD
         S.nslots = sb;
         S.ncoef = cr;
-
-        // ---- A. first 64 coefficient words (contiguous for the group; host-validated) ----
         const uint32_t cw0 = lane < S.ncoef ? coefs[S.coef0 + lane] : 0u;
 
-        // ---- B. issue the MC loads of every item this lane owns (consumed in stage F) ----
-        Tap tf[IPL], tb[IPL];
-#pragma unroll
-        for (int j = 0; j < IPL; j++) {
-            const int it = lane + 64 * j;
-            int k, plane, px, py;
-            item_coords<CF, G>(it < NIT ? it : 0, k, plane, px, py);
-            const uint32_t fl = pick<G>(S.flags, k);
-            const bool intra = (fl & MP2VG_MB_INTRA) || it >= NIT || (ABL & 2);
-            const bool bwd = fl & MP2VG_MB_BWD;
-            const bool fwd = !intra && ((fl & MP2VG_MB_FWD) || !bwd);
-            const bool field = fl & MP2VG_MB_FIELD_MC;
-            const int pw = plane == 0 ? 16 : F::CW;
-            const int phm = plane == 0 ? 16 : F::CH;
-            const int gx = (int)pick<G>(S.mbx, k) * pw + px;
-            const int mbyb = (int)pick<G>(S.mby, k) * phm;
-            const int r = field ? (py & 1) : 0;
-            const int stride = geo.stride[plane];
-            tf[j] = Tap{0, 0, 0, 0};
-            tb[j] = Tap{0, 0, 0, 0};
-            if (fwd) {
-                uint32_t mvw = (r ? pick<G>(S.mv[2], k) : pick<G>(S.mv[0], k));
-                int o0, o1, sh, hxy;
-                tap_geometry<CF>(mvw, plane, gx, py, mbyb, field, (fl >> (8 + 2 * r)) & 1, stride, geo.ph[plane], o0, o1, sh, hxy);
-                tf[j] = issue_tap(ref_fwd + geo.plane_off[plane], o0, o1, hxy);
-            }
-            if (!intra && bwd) {
-                uint32_t mvw = (r ? pick<G>(S.mv[3], k) : pick<G>(S.mv[1], k));
-                int o0, o1, sh, hxy;
-                tap_geometry<CF>(mvw, plane, gx, py, mbyb, field, (fl >> (9 + 2 * r)) & 1, stride, geo.ph[plane], o0, o1, sh, hxy);
-                tb[j] = issue_tap(ref_bwd + geo.plane_off[plane], o0, o1, hxy);
-            }
-        }
+        // ---- B. reference-row loads of every pixel row (consumed in E) ----
+        RowTap<4> t0f, t0b;   // luma rows
+        RowTap<NWC> t1f, t1b;  // chroma rows (4:2:0: Cb + Cr; else Cb)
+        RowTap<NWC> t2f, t2b;  // Cr rows (4:2:2 / 4:4:4)
+        issue_pass<CF, 0, 4>(S, lane, geo, ref_fwd, ref_bwd, t0f, t0b, ABL & 2);
+        issue_pass<CF, 1, NWC>(S, lane, geo, ref_fwd, ref_bwd, t1f, t1b, ABL & 2);
+        if (CF != 1) issue_pass<CF, 2, NWC>(S, lane, geo, ref_fwd, ref_bwd, t2f, t2b, ABL & 2);
 
-        // ---- C. slot map + dequant/mismatch parity (parse_block, mb_decoder.cpp:74-155) ----
+        // ---- C. slot map + dequant (parse_block, mb_decoder.cpp:74-155) ----
         if (lane < MAXS) {
             const int k = lane / NB, bb = lane % NB;
-            const uint32_t cbpk = pick<G>(S.cbp, k);
-            if (cbpk & (1u << bb)) s_map[wave][pick<G>(S.slot_base, k) + __builtin_popcount(cbpk & ((1u << bb) - 1))] = (uint8_t)(k * 16 + bb);
+            const uint32_t cbpk = pick(S.cbp, k);
+            if (cbpk & (1u << bb))
+                s_map[wave][(int)pick(S.slot_base, k) + __builtin_popcount(cbpk & ((1u << bb) - 1))] = (uint8_t)(k * 16 + bb);
         }
         for (int k0 = 0; k0 < ((ABL & 4) ? 0 : S.ncoef); k0 += 64) {
             const int w_idx = k0 + lane;
@@ -368,13 +479,13 @@ __global__ __launch_bounds__(256) void recon_kernel(const mp2vg_picture_t* __res
             if (w_idx >= S.ncoef) continue;
             int k = 0;
 #pragma unroll
-            for (int i = 1; i < G; i++) k += (w_idx >= S.coef_rel[i]) ? 1 : 0;
-            const uint32_t cbpk = pick<G>(S.cbp, k);
+            for (int i = 1; i < G; i++) k += (w_idx >= (int)S.coef_rel[i]) ? 1 : 0;
+            const uint32_t cbpk = pick(S.cbp, k);
             const int bb = (w >> 22) & 15;
             if (bb >= NB || !(cbpk & (1u << bb))) continue;  // host validation rejects these
-            const int slot = pick<G>(S.slot_base, k) + __builtin_popcount(cbpk & ((1u << bb) - 1));
-            const bool intra = pick<G>(S.flags, k) & MP2VG_MB_INTRA;
-            const int qs = (int)pick<G>(S.qs, k);
+            const int slot = (int)pick(S.slot_base, k) + __builtin_popcount(cbpk & ((1u << bb) - 1));
+            const bool intra = pick(S.flags, k) & MP2VG_MB_INTRA;
+            const int qs = (int)pick(S.qs, k);
             const int i = (w >> 16) & 63;
             const int level = (short)(w & 0xffff);
             if (w & MP2VG_COEF_DC) {  // QFS[0] = dc << (3 - prec), outside the parity sum (:160)
@@ -398,106 +509,64 @@ __global__ __launch_bounds__(256) void recon_kernel(const mp2vg_picture_t* __res
                 pos = s_scan[i];
             }
             s_blk[wave][slot][pos] = v;
-            if (v & 1) atomicXor(&s_par[wave][slot], 1);
-        }
-        wave_sync();
-        for (int s = lane; s < S.nslots; s += 64) {  // qfs[63] ^= !(sum & 1)   (:150-152)
-            s_blk[wave][s][63] ^= (short)((s_par[wave][s] & 1) ^ 1);
-            s_par[wave][s] = 0;
         }
         wave_sync();
 
-        // ---- D. IDCT pass 1 (idct_sse2.hpp:102-103): lane (slot, v) transforms coefficient row v
-        //         over u; output transposed IN PLACE ([x][v]) — the whole 8-lane block is read by
-        //         one ds_read instruction before any lane writes.
-        for (int t = lane; t < ((ABL & 1) ? 0 : S.nslots * 8); t += 64) {
-            const int slot = t >> 3, v = t & 7;
-            short s[8];
-            const uint4 row = *(const uint4*)&s_blk[wave][slot][v * 8];
-            s[0] = (short)(row.x & 0xffff); s[1] = (short)(row.x >> 16);
-            s[2] = (short)(row.y & 0xffff); s[3] = (short)(row.y >> 16);
-            s[4] = (short)(row.z & 0xffff); s[5] = (short)(row.z >> 16);
-            s[6] = (short)(row.w & 0xffff); s[7] = (short)(row.w >> 16);
+        // ---- D. IDCT pass 1 (idct_sse2.hpp:102-103): lane (slot, v, v+1) transforms coefficient
+        //         rows v, v+1 over u.  Mismatch control (mb_decoder.cpp:150-152; intra DC
+        //         excluded, :76) is folded in: the block parity is reduced over the slot's 4
+        //         lanes with ds_swizzle and applied to QFS[63] (row 7, u 7) before the
+        //         transform.  Output transposed in place ([x][v]): the block is read by one
+        //         ds_read instruction before any lane writes it.
+        for (int t = lane; t < ((ABL & 1) ? 0 : S.nslots * 4); t += 64) {
+            const int slot = t >> 2, v = (t & 3) * 2;
+            uint4 ra = *(const uint4*)&s_blk[wave][slot][v * 8];
+            uint4 rb = *(const uint4*)&s_blk[wave][slot][v * 8 + 8];
+            const int k = s_map[wave][slot] >> 4;
+            const bool intra = pick(S.flags, k) & MP2VG_MB_INTRA;
+            uint32_t par = (ra.x ^ ra.y ^ ra.z ^ ra.w ^ rb.x ^ rb.y ^ rb.z ^ rb.w) & 0x00010001u;
+            if (v == 0 && intra) par ^= ra.x & 1u;  // DC excluded
+            par = (par ^ (par >> 16)) & 1u;
+            par ^= (uint32_t)__builtin_amdgcn_ds_swizzle((int)par, 0x041F);  // xor lane 1
+            par ^= (uint32_t)__builtin_amdgcn_ds_swizzle((int)par, 0x081F);  // xor lane 2
+            if (v == 6) rb.w ^= (par ^ 1u) << 16;  // sum even -> toggle the LSB of QFS[63]
+            short2_t s[8];
+            interleave(ra, rb, s);
             idct_1d(s);
 #pragma unroll
-            for (int x = 0; x < 8; x++) s_blk[wave][slot][x * 8 + v] = s[x];
+            for (int x = 0; x < 8; x++) *(short2_t*)&s_blk[wave][slot][x * 8 + v] = s[x];
         }
         wave_sync();
-        // pass 2 (:104-108): lane (slot, x) transforms column x over v; >>6 -> residual image in
-        // the MB's dct_type placement (:166-196); the block area is zeroed for the next group
-        for (int t = lane; t < ((ABL & 1) ? 0 : S.nslots * 8); t += 64) {
-            const int slot = t >> 3, x = t & 7;
-            short s[8];
-            const uint4 row = *(const uint4*)&s_blk[wave][slot][x * 8];
+        // pass 2 (:104-108): lane (slot, x, x+2) transforms columns x, x+2 over v; >>6 -> residual
+        // image in the MB's dct_type placement (:166-196); the block area is zeroed for the next
+        // group
+        for (int t = lane; t < ((ABL & 1) ? 0 : S.nslots * 4); t += 64) {
+            const int slot = t >> 2, xq = t & 3;
+            const int x = (xq & 1) | ((xq & 2) << 1);  // 0, 1, 4, 5
+            const uint4 ra = *(const uint4*)&s_blk[wave][slot][x * 8];
+            const uint4 rb = *(const uint4*)&s_blk[wave][slot][x * 8 + 16];
             *(uint4*)&s_blk[wave][slot][x * 8] = make_uint4(0, 0, 0, 0);
-            s[0] = (short)(row.x & 0xffff); s[1] = (short)(row.x >> 16);
-            s[2] = (short)(row.y & 0xffff); s[3] = (short)(row.y >> 16);
-            s[4] = (short)(row.z & 0xffff); s[5] = (short)(row.z >> 16);
-            s[6] = (short)(row.w & 0xffff); s[7] = (short)(row.w >> 16);
+            *(uint4*)&s_blk[wave][slot][x * 8 + 16] = make_uint4(0, 0, 0, 0);
+            short2_t s[8];
+            interleave(ra, rb, s);
             idct_1d(s);
             const int kb = s_map[wave][slot];
             const int k = kb >> 4, bb = kb & 15;
-            const bool dctf = pick<G>(S.flags, k) & MP2VG_MB_DCT_FIELD;
+            const bool dctf = pick(S.flags, k) & MP2VG_MB_DCT_FIELD;
             int plane, x0, y0, ys;
             block_origin<CF>(bb, dctf, plane, x0, y0, ys);
-            short* res = &s_res[wave][k][RL::base(plane)];
+            short* res = &s_res[wave][k * RL::SIZE + RL::base(plane)];
             const int rw = RL::width(plane);
+            const int xp = RL::pos(x0 + x);  // (x, x+2) -> (xp, xp+1)
 #pragma unroll
-            for (int y = 0; y < 8; y++) res[(y0 + y * ys) * rw + x0 + x] = (short)(s[y] >> 6);
+            for (int y = 0; y < 8; y++) *(short2_t*)&res[(y0 + y * ys) * rw + xp] = s[y] >> (short)6;
         }
         wave_sync();
 
-        // ---- E. prediction (+ residual, clamp) and one 4-byte store per item ----
-#pragma unroll
-        for (int j = 0; j < IPL; j++) {
-            const int it = lane + 64 * j;
-            if (it >= NIT) continue;
-            int k, plane, px, py;
-            item_coords<CF, G>(it, k, plane, px, py);
-            if (k >= ng) continue;
-            const uint32_t fl = pick<G>(S.flags, k);
-            const bool intra = fl & MP2VG_MB_INTRA;
-            const bool bwd = fl & MP2VG_MB_BWD;
-            const bool fwd = !intra && ((fl & MP2VG_MB_FWD) || !bwd);
-            const bool field = fl & MP2VG_MB_FIELD_MC;
-            const int pw = plane == 0 ? 16 : F::CW;
-            const int phm = plane == 0 ? 16 : F::CH;
-            const int mbx = (int)pick<G>(S.mbx, k), mby = (int)pick<G>(S.mby, k);
-            const int stride = geo.stride[plane];
-            const int r = field ? (py & 1) : 0;
-            uint32_t pred = 0;
-            if (!intra) {
-                uint32_t pf = 0, pb = 0;
-                if (fwd) {
-                    int o0, o1, sh, hxy;
-                    tap_geometry<CF>((r ? pick<G>(S.mv[2], k) : pick<G>(S.mv[0], k)), plane, mbx * pw + px, py, mby * phm,
-                                     field, (fl >> (8 + 2 * r)) & 1, stride, geo.ph[plane], o0, o1, sh, hxy);
-                    pf = finish_tap(tf[j], sh, hxy);
-                }
-                if (bwd) {
-                    int o0, o1, sh, hxy;
-                    tap_geometry<CF>((r ? pick<G>(S.mv[3], k) : pick<G>(S.mv[1], k)), plane, mbx * pw + px, py, mby * phm,
-                                     field, (fl >> (9 + 2 * r)) & 1, stride, geo.ph[plane], o0, o1, sh, hxy);
-                    pb = finish_tap(tb[j], sh, hxy);
-                }
-                pred = (fwd && bwd) ? avg4(pf, pb) : (fwd ? pf : pb);  // mc_sse2.hpp:78-84
-            }
-            const int bb = block_of<CF>(plane, px, py, fl & MP2VG_MB_DCT_FIELD);
-            uint32_t out = pred;
-            if (pick<G>(S.cbp, k) & (1u << bb)) {  // put: packus(res); add: packus(adds(pred,res))
-                const uint2 rr = *(const uint2*)&s_res[wave][k][RL::base(plane) + py * RL::width(plane) + px];
-                int q0 = (int)(pred & 255) + (short)(rr.x & 0xffff);
-                int q1 = (int)((pred >> 8) & 255) + (short)(rr.x >> 16);
-                int q2 = (int)((pred >> 16) & 255) + (short)(rr.y & 0xffff);
-                int q3 = (int)(pred >> 24) + (short)(rr.y >> 16);
-                q0 = min(max(q0, 0), 255);
-                q1 = min(max(q1, 0), 255);
-                q2 = min(max(q2, 0), 255);
-                q3 = min(max(q3, 0), 255);
-                out = (uint32_t)q0 | ((uint32_t)q1 << 8) | ((uint32_t)q2 << 16) | ((uint32_t)q3 << 24);
-            }
-            if (ABL & 8) asm volatile("" ::"v"(out)); else *(uint32_t*)(dst_slot + geo.plane_off[plane] + (size_t)(mby * phm + py) * stride + mbx * pw + px) = out;
-        }
+        // ---- E. prediction + residual, one row store per lane ----
+        finish_pass<CF, 0, 4, ABL>(S, ng, lane, geo, dst_slot, s_res[wave], t0f, t0b);
+        finish_pass<CF, 1, NWC, ABL>(S, ng, lane, geo, dst_slot, s_res[wave], t1f, t1b);
+        if (CF != 1) finish_pass<CF, 2, NWC, ABL>(S, ng, lane, geo, dst_slot, s_res[wave], t2f, t2b);
         wave_sync();
     }
 }
@@ -540,8 +609,6 @@ __global__ void digest_kernel(const uint8_t* __restrict__ pool, uint64_t slot_by
     if ((threadIdx.x & 63) == 0) atomicAdd(&out[si], (unsigned long long)acc);
 }
 
-constexpr int kGroup = 2;
-
 hipError_t launch_recon(int cf, const KArgs& a, hipStream_t stream) {
     dim3 grid(a.nslices), block(256);
     Geo g;
@@ -557,7 +624,7 @@ hipError_t launch_recon(int cf, const KArgs& a, hipStream_t stream) {
     static const int ablate = getenv("MP2VG_ABLATE") ? atoi(getenv("MP2VG_ABLATE")) : 0;
     if (cf == 1 && ablate) {
 #define ABL_CASE(v) \
-    case v: hipLaunchKernelGGL((recon_kernel<1, kGroup, v>), grid, block, 0, stream, a.pics, mb, a.coefs, a.slices, a.pool, g, a.slice_base, a.nslices); break;
+    case v: hipLaunchKernelGGL((recon_kernel<1, v>), grid, block, 0, stream, a.pics, mb, a.coefs, a.slices, a.pool, g, a.slice_base, a.nslices); break;
         switch (ablate) {
             ABL_CASE(1) ABL_CASE(2) ABL_CASE(3) ABL_CASE(4) ABL_CASE(8) ABL_CASE(15)
         default: return hipErrorInvalidValue;
@@ -566,9 +633,9 @@ hipError_t launch_recon(int cf, const KArgs& a, hipStream_t stream) {
         return hipGetLastError();
     }
     switch (cf) {
-    case 1: hipLaunchKernelGGL((recon_kernel<1, kGroup>), grid, block, 0, stream, a.pics, mb, a.coefs, a.slices, a.pool, g, a.slice_base, a.nslices); break;
-    case 2: hipLaunchKernelGGL((recon_kernel<2, kGroup>), grid, block, 0, stream, a.pics, mb, a.coefs, a.slices, a.pool, g, a.slice_base, a.nslices); break;
-    case 3: hipLaunchKernelGGL((recon_kernel<3, kGroup>), grid, block, 0, stream, a.pics, mb, a.coefs, a.slices, a.pool, g, a.slice_base, a.nslices); break;
+    case 1: hipLaunchKernelGGL((recon_kernel<1>), grid, block, 0, stream, a.pics, mb, a.coefs, a.slices, a.pool, g, a.slice_base, a.nslices); break;
+    case 2: hipLaunchKernelGGL((recon_kernel<2>), grid, block, 0, stream, a.pics, mb, a.coefs, a.slices, a.pool, g, a.slice_base, a.nslices); break;
+    case 3: hipLaunchKernelGGL((recon_kernel<3>), grid, block, 0, stream, a.pics, mb, a.coefs, a.slices, a.pool, g, a.slice_base, a.nslices); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
