@@ -150,7 +150,9 @@ int  mp2vg_download_slot(mp2vg_ctx_t* ctx, int32_t slot, uint8_t* dst_planes[3],
                          const int32_t dst_stride[3]);
 /* raw device pointer of a slot (for in-HBM consumers such as a digest kernel or RCCL) */
 int  mp2vg_slot_device_ptr(mp2vg_ctx_t* ctx, int32_t slot, void** dptr);
-/* 64-bit FNV-1a digest of each listed slot's visible planes, computed on device */
+/* 64-bit order-independent digest of each listed slot's visible planes, computed on device:
+ * sum over visible dwords d of (mix64((row << 32) | byte_x) ^ d) mod 2^64 (numpy twin:
+ * tiny_mp2v_dec_amd.records.planes_digest) */
 int  mp2vg_slot_digests(mp2vg_ctx_t* ctx, const int32_t* slots, int32_t n, uint64_t* out);
 
 /* ---- host record emitter -------------------------------------------------------------- */

@@ -9,7 +9,7 @@ import os
 import numpy as np
 
 PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG, "_build", "libmp2vg.so")
+LIB_PATH = os.environ.get("MP2VG_LIB") or os.path.join(PKG, "_build", "libmp2vg.so")  # override: dev A/B builds
 
 # ---- record dtypes (must match include/mp2vg.h) ------------------------------------------
 MB_DTYPE = np.dtype([("x", "<u2"), ("y", "<u2"), ("flags", "<u2"), ("cbp", "<u2"), ("qscale", "u1"),
