@@ -30,8 +30,16 @@ struct SliceDesc {
     uint32_t reserved;
 };
 
+// one kernel launch: a slice range of one dependency level and one motion-compensation mode
+// (0: I pictures, 1: P, forward only, 2: B)
+struct Launch {
+    uint32_t begin, end;
+    int mcm;
+};
+
 // per-launch geometry, passed by value
 struct Geo {
+    uint8_t* sink;  // 16+ writable, readable bytes outside every slot: dummy loads and stores
     uint64_t slot_bytes;
     uint64_t plane_off[3];
     int32_t stride[3];
@@ -44,6 +52,7 @@ struct KArgs {
     const uint32_t* coefs;
     const SliceDesc* slices;
     uint8_t* pool;
+    uint8_t* sink;
     uint64_t slot_bytes;
     uint64_t plane_off[3];
     int32_t stride[3];

@@ -17,7 +17,7 @@
 #include "syntax.h"
 
 namespace mp2vg {
-hipError_t launch_recon(int cf, const KArgs& a, hipStream_t stream);
+hipError_t launch_recon(int cf, int mcm, const KArgs& a, hipStream_t stream);
 hipError_t launch_digest(const uint8_t* pool, uint64_t slot_bytes, const int32_t* d_slots, int n,
                          const uint64_t off[3], const int32_t stride[3], const int32_t w[3],
                          const int32_t h[3], unsigned long long* d_out, hipStream_t stream);
@@ -34,7 +34,10 @@ using namespace mp2vg;
         }                                                                                  \
     } while (0)
 
-static constexpr size_t kPoolPad = 4096;       // slack after the last slot (load5 reads 4 B past)
+static constexpr size_t kPoolPad = 4096;       // slack after the last slot: clamped row over-reads, and the
+                                               // kernel's dummy load / store sink at +2048 (kSinkOff)
+static constexpr size_t kSinkOff = 2048;
+static constexpr size_t kCoefPad = 128;        // the kernel prefetches 128 coefficient words per MB group
 static constexpr size_t kStageBytes = 32u << 20;
 static constexpr size_t kMbPad = 16;  // >= the kernel's MB group size
 
@@ -53,7 +56,7 @@ struct mp2vg_ctx {
     size_t cap_coefs = 0;
     SliceDesc* d_slices = nullptr;
     size_t cap_slices = 0;
-    std::vector<uint32_t> level_begin;  // slice ranges per dependency level
+    std::vector<Launch> launches;  // slice ranges per (dependency level, picture type)
     bool batch_ready = false;
     int32_t batch_pics = 0;
 
@@ -163,7 +166,7 @@ extern "C" int mp2vg_reserve_slots(mp2vg_ctx_t* c, int32_t nslots) {
 // Validate the batch so no kernel access can leave its buffers, and compute dependency levels.
 static int plan_batch(mp2vg_ctx_t* c, const mp2vg_picture_t* pics, int32_t npics, const mp2vg_mb_t* mbs,
                       uint64_t nmbs, uint64_t ncoefs, std::vector<SliceDesc>& slices,
-                      std::vector<uint32_t>& level_begin) {
+                      std::vector<Launch>& launches) {
     const int mbw = c->cfg.width / 16, mbh = c->cfg.height / 16;
     const int nb = c->g.nblocks;
     std::vector<int> level(npics, 0);
@@ -234,16 +237,25 @@ static int plan_batch(mp2vg_ctx_t* c, const mp2vg_picture_t* pics, int32_t npics
         max_read[P.dst_slot] = -1;
         maxlevel = std::max(maxlevel, lv);
     }
-    level_begin.assign(maxlevel + 2, 0);
-    std::vector<std::vector<int>> bylevel(maxlevel + 1);
-    for (int p = 0; p < npics; p++) bylevel[level[p]].push_back(p);
-    slices.clear();
-    for (int L = 0; L <= maxlevel; L++) {
-        level_begin[L] = (uint32_t)slices.size();
-        for (int p : bylevel[L])
-            for (int r = 0; r < mbh; r++) slices.push_back({(uint32_t)p, pics[p].mb_first + (uint32_t)(r * mbw), (uint32_t)mbw, 0});
+    // one launch per (level, motion-compensation mode): I pictures (none), P (forward only),
+    // B (both directions) each run a kernel specialised -- and register-allocated -- for it
+    std::vector<std::vector<int>> bylevel(3 * (maxlevel + 1));
+    for (int p = 0; p < npics; p++) {
+        const int pct = pics[p].picture_coding_type;
+        bylevel[3 * level[p] + (pct == 1 ? 0 : (pct == 2 ? 1 : 2))].push_back(p);
     }
-    level_begin[maxlevel + 1] = (uint32_t)slices.size();
+    slices.clear();
+    launches.clear();
+    for (size_t q = 0; q < bylevel.size(); q++) {
+        if (bylevel[q].empty()) continue;
+        Launch l;
+        l.begin = (uint32_t)slices.size();
+        for (int p : bylevel[q])
+            for (int r = 0; r < mbh; r++) slices.push_back({(uint32_t)p, pics[p].mb_first + (uint32_t)(r * mbw), (uint32_t)mbw, 0});
+        l.end = (uint32_t)slices.size();
+        l.mcm = (int)(q % 3);
+        launches.push_back(l);
+    }
     return MP2VG_OK;
 }
 
@@ -254,20 +266,20 @@ extern "C" int mp2vg_batch_upload(mp2vg_ctx_t* c, const mp2vg_picture_t* pics, i
     HIPCHK(hipSetDevice(c->cfg.device));
     c->batch_ready = false;
     std::vector<SliceDesc> slices;
-    std::vector<uint32_t> lb;
+    std::vector<Launch> lb;
     int rc = plan_batch(c, pics, npics, mbs, nmbs, ncoefs, slices, lb);
     if (rc != MP2VG_OK) return rc;
     HIPCHK(hipStreamSynchronize(c->stream));
     if ((rc = grow(c->d_pics, c->cap_pics, (size_t)npics)) != MP2VG_OK) return rc;
-    // the kernel reads whole MB groups with scalar loads: pad the record array
     if ((rc = grow(c->d_mbs, c->cap_mbs, (size_t)nmbs + kMbPad)) != MP2VG_OK) return rc;
-    if ((rc = grow(c->d_coefs, c->cap_coefs, (size_t)std::max<uint64_t>(ncoefs, 1))) != MP2VG_OK) return rc;
+    // the kernel loads 128 words from the first coefficient of each MB group unconditionally
+    if ((rc = grow(c->d_coefs, c->cap_coefs, (size_t)ncoefs + kCoefPad)) != MP2VG_OK) return rc;
     if ((rc = grow(c->d_slices, c->cap_slices, slices.size())) != MP2VG_OK) return rc;
     if ((rc = upload(c, c->d_pics, pics, sizeof(mp2vg_picture_t) * npics)) != MP2VG_OK) return rc;
     if ((rc = upload(c, c->d_mbs, mbs, sizeof(mp2vg_mb_t) * nmbs)) != MP2VG_OK) return rc;
     if (ncoefs && (rc = upload(c, c->d_coefs, coefs, sizeof(uint32_t) * ncoefs)) != MP2VG_OK) return rc;
     if ((rc = upload(c, c->d_slices, slices.data(), sizeof(SliceDesc) * slices.size())) != MP2VG_OK) return rc;
-    c->level_begin = lb;
+    c->launches = lb;
     c->batch_pics = npics;
     c->batch_ready = true;
     return MP2VG_OK;
@@ -280,7 +292,7 @@ extern "C" int mp2vg_batch_decode(mp2vg_ctx_t* c) {
         return MP2VG_E_STATE;
     }
     HIPCHK(hipSetDevice(c->cfg.device));
-    int nl = (int)c->level_begin.size() - 1;
+    int nl = (int)c->launches.size();
     while ((int)c->ev.size() < 2 * nl) {
         hipEvent_t e;
         HIPCHK(hipEventCreate(&e));
@@ -293,6 +305,7 @@ extern "C" int mp2vg_batch_decode(mp2vg_ctx_t* c) {
     a.coefs = c->d_coefs;
     a.slices = c->d_slices;
     a.pool = c->d_pool;
+    a.sink = c->d_pool + (size_t)c->g.slot_bytes * c->nslots + kSinkOff;
     a.slot_bytes = c->g.slot_bytes;
     for (int i = 0; i < 3; i++) {
         a.plane_off[i] = c->g.plane_off[i];
@@ -300,10 +313,10 @@ extern "C" int mp2vg_batch_decode(mp2vg_ctx_t* c) {
         a.ph[i] = c->g.ph[i];
     }
     for (int L = 0; L < nl; L++) {
-        a.slice_base = c->level_begin[L];
-        a.nslices = c->level_begin[L + 1] - c->level_begin[L];
+        a.slice_base = c->launches[L].begin;
+        a.nslices = c->launches[L].end - c->launches[L].begin;
         HIPCHK(hipEventRecord(c->ev[2 * L], c->stream));
-        if (a.nslices) HIPCHK(launch_recon(c->g.cf, a, c->stream));
+        if (a.nslices) HIPCHK(launch_recon(c->g.cf, c->launches[L].mcm, a, c->stream));
         HIPCHK(hipEventRecord(c->ev[2 * L + 1], c->stream));
     }
     c->nlaunch = nl;
