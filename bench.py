@@ -142,11 +142,12 @@ def main():
 
     barrier()
     ctx.synchronize()
-    kernel_ms = []
+    kernel_ms, batch_ms = [], []
     t0 = time.perf_counter()
     for _ in range(args.steps):
         ctx.decode()
-        kernel_ms.append(ctx.launch_times_ms())  # HIP events on the launch stream
+        kernel_ms.append(ctx.launch_times_ms())  # HIP events on each launch's stream
+        batch_ms.append(ctx.batch_time_ms())  # first launch start -> last launch end
     ctx.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
@@ -169,7 +170,9 @@ def main():
     frames_total = parsed.npics * world * args.steps
     ms_per_step = elapsed * 1000.0 / args.steps
     per_launch = [x for step in kernel_ms for x in step]
-    kernel_step_ms = float(np.mean([sum(s) for s in kernel_ms]))
+    # launches of one dependency level overlap on two streams: the kernel time of a step is the
+    # device span of the batch, not the sum of the launches
+    kernel_step_ms = float(np.mean(batch_ms))
     achieved = alg_bytes / (kernel_step_ms / 1000.0) / 1e9
     result = {
         "metric": BASELINE_METRIC,
@@ -193,7 +196,8 @@ def main():
                      "kernel": "mp2vg::recon_kernel", "launches_per_step": len(kernel_ms[0]),
                      "avg_launch_ms": round(float(np.mean(per_launch)), 4),
                      "algorithmic_bytes_per_step": int(alg_bytes), "bytes_breakdown": parts,
-                     "kernel_ms_per_step": round(kernel_step_ms, 4)},
+                     "kernel_ms_per_step": round(kernel_step_ms, 4),
+                     "sum_launch_ms_per_step": round(float(np.mean([sum(s) for s in kernel_ms])), 4)},
         "frame_digest_of_digests": int(np.bitwise_xor.reduce(np.concatenate(gathered))),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -144,6 +144,8 @@ int  mp2vg_batch_decode(mp2vg_ctx_t* ctx);
 int  mp2vg_synchronize(mp2vg_ctx_t* ctx);
 /* number of kernel launches of the last mp2vg_batch_decode and their device times (ms) */
 int  mp2vg_last_launch_times(mp2vg_ctx_t* ctx, float* ms, int32_t max, int32_t* count);
+/* device time (ms) of the whole last mp2vg_batch_decode: first launch start to last launch end */
+int  mp2vg_last_batch_time(mp2vg_ctx_t* ctx, float* ms);
 /* copy one frame slot to host planes (each plane written width x height, tightly packed if
  * dst_stride is 0); synchronous */
 int  mp2vg_download_slot(mp2vg_ctx_t* ctx, int32_t slot, uint8_t* dst_planes[3],

@@ -35,6 +35,7 @@ struct SliceDesc {
 struct Launch {
     uint32_t begin, end;
     int mcm;
+    int level;  // dependency level: launches of one level may run concurrently
 };
 
 // per-launch geometry, passed by value

@@ -115,6 +115,12 @@ class DeviceContext:
         check(lib().mp2vg_last_launch_times(self.h, buf, 256, ctypes.byref(n)), "last_launch_times")
         return list(buf[:min(n.value, 256)])
 
+    def batch_time_ms(self):
+        """Device time of the whole last batch_decode (first launch start -> last launch end)."""
+        ms = ctypes.c_float()
+        check(lib().mp2vg_last_batch_time(self.h, ctypes.byref(ms)), "last_batch_time")
+        return ms.value
+
     def download(self, slot):
         """Visible planes of one slot: [Y, U, V] numpy arrays (height x width)."""
         planes = [np.empty((self.ph[i], self.pw[i]), np.uint8) for i in range(3)]

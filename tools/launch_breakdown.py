@@ -31,7 +31,11 @@ def main():
             d.decode()
             d.synchronize()
             times.append(d.launch_times_ms())
+            spans = getattr(main, "spans", [])
+            spans.append(d.batch_time_ms())
+            main.spans = spans
         t = np.array(times[1:]).mean(axis=0)
+        print(f"batch span {np.mean(main.spans[1:]):.4f} ms")
     # reconstruct the runtime's launch order: by dependency level, then I / P / B
     pct = p.pics["picture_coding_type"]
     mbs_per_pic = len(p.mbs) // p.npics
