@@ -98,6 +98,19 @@ def cpu_baseline(es, width, height, cf, frames):
             "sample": f"oracle C restatement over the bench records ({parsed.npics} frames), no parse"}
 
 
+def profiled_traffic(config, gops):
+    """HBM bytes per step of this exact workload from the committed rocprofv3 PMC summary
+    (profiles/traffic_<config>_g<gops>.json, written by tools/prof_summary.py --json from
+    tools/profile.sh's separate FETCH_SIZE / WRITE_SIZE passes of this bench command), or None."""
+    path = os.path.join(REPO, "profiles", f"traffic_{config}_g{gops}.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as fh:
+        d = json.load(fh)
+    d["source"] = f"profiles/{os.path.basename(path)} ({d.get('tag')})"
+    return d
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -167,6 +180,7 @@ def main():
         dist.all_gather(outs, d)
         gathered = [o.cpu().numpy().view(np.uint64) for o in outs]
 
+    traffic = profiled_traffic(args.config, gops)
     frames_total = parsed.npics * world * args.steps
     ms_per_step = elapsed * 1000.0 / args.steps
     per_launch = [x for step in kernel_ms for x in step]
@@ -192,7 +206,8 @@ def main():
                    "frames_per_gpu_per_step": parsed.npics, "global_batch_frames": parsed.npics * world,
                    "parallelism": f"gop-shard x{world}"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic["traffic_bytes_per_step"] if traffic else None,
+                     "traffic_unit": "bytes/step (HBM, PMC)", "traffic_source": traffic["source"] if traffic else None,
                      "kernel": "mp2vg::recon_kernel", "launches_per_step": len(kernel_ms[0]),
                      "avg_launch_ms": round(float(np.mean(per_launch)), 4),
                      "algorithmic_bytes_per_step": int(alg_bytes), "bytes_breakdown": parts,

@@ -33,6 +33,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("tag")
     ap.add_argument("--out")
+    ap.add_argument("--json", help="write HBM traffic per bench step (bytes) for bench.py's roofline.traffic")
+    ap.add_argument("--steps-total", type=int, default=12, help="bench steps + warmup steps profiled")
+    ap.add_argument("--config", default="c2")
+    ap.add_argument("--gops", type=int, default=64)
     args = ap.parse_args()
     d = os.path.join(REPO, "gpurun_out", f"prof_{args.tag}")
     lines = [f"# rocprofv3 summary: {args.tag}", ""]
@@ -72,6 +76,19 @@ def main():
                          f"{(2 * f + w) / 1e6:.1f} MB")
             if durs:
                 lines.append(f"kernel-trace mean duration {statistics.mean(durs) / 1e3:.1f} us over {len(durs)} dispatches")
+            fsum = sum(counters["FETCH_SIZE"]) * 1024 * 2 / args.steps_total
+            wsum = sum(counters["WRITE_SIZE"]) * 1024 / args.steps_total
+            lines.append(f"per bench step ({args.steps_total} steps profiled): FETCH x2 {fsum / 1e9:.3f} GB + WRITE "
+                         f"{wsum / 1e9:.3f} GB = {(fsum + wsum) / 1e9:.3f} GB")
+            if args.json:
+                import json
+                with open(args.json, "w") as fh:
+                    json.dump({"tag": args.tag, "config": args.config, "gops": args.gops,
+                               "traffic_bytes_per_step": int(fsum + wsum), "fetch_x2_bytes_per_step": int(fsum),
+                               "write_bytes_per_step": int(wsum),
+                               "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes (KiB), "
+                                         "FETCH x2 (gfx950 wide-read correction, MI355X_MICROARCH.md), summed over "
+                                         "the recon_kernel dispatches of the profiled bench run / steps"}, fh, indent=1)
         lines.append("")
     text = "\n".join(lines)
     print(text)
