@@ -91,10 +91,10 @@ def random_batch(width, height, cf, npics, seed, field=True, big=False):
                     continue
                 pos = 0
                 if intra:
-                    coefs.append(R._lib.coef_pack(int(rng.integers(0, 2048)), 0, b, COEF_DC))
+                    coefs.append(R._lib.coef_pack(int(rng.integers(0, 2048)), 0, b, COEF_DC, m["x"]))
                     pos = 1
                 elif rng.random() < 0.3:
-                    coefs.append(R._lib.coef_pack(int(rng.choice([-1, 1])), 0, b, COEF_FIRST1S))
+                    coefs.append(R._lib.coef_pack(int(rng.choice([-1, 1])), 0, b, COEF_FIRST1S, m["x"]))
                     pos = 1
                 ncoef = int(rng.integers(0 if intra else 1, 20))
                 for _ in range(ncoef):
@@ -102,7 +102,7 @@ def random_batch(width, height, cf, npics, seed, field=True, big=False):
                     if pos > 63:
                         break
                     lvl = int(rng.integers(-2048, 2048)) if (big and rng.random() < 0.3) else int(rng.integers(-40, 41))
-                    coefs.append(R._lib.coef_pack(lvl, pos, b))
+                    coefs.append(R._lib.coef_pack(lvl, pos, b, 0, m["x"]))
                     pos += 1
             m["ncoef"] = len(coefs) - m["coef_off"]
     return pics, mbs, np.array(coefs, dtype=np.uint32)

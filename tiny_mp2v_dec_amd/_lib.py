@@ -29,9 +29,10 @@ def mb_fs_bit(r, s):
     return 1 << (8 + 2 * r + s)
 
 
-def coef_pack(level, pos, block, flags=0):
+def coef_pack(level, pos, block, flags=0, mbx=0):
+    """Coefficient word (include/mp2vg.h); mbx = the MB's column (bits 28-30 carry mbx & 7)."""
     return (np.uint32(np.int64(level) & 0xFFFF) | np.uint32(pos << 16) | np.uint32(block << 22) |
-            np.uint32(flags))
+            np.uint32(flags) | np.uint32((int(mbx) & 7) << 28))
 
 
 STATUS = {0: "ok", -1: "invalid argument", -2: "unsupported stream", -3: "HIP error", -4: "out of memory",

@@ -330,14 +330,14 @@ void parse_slice(const Ctx& C, const PicWork& P, const SliceJob& job, mp2vg_mb_t
                 }
                 dc_pred[pidx] = (uint16_t)(dc_pred[pidx] + diff);
                 int16_t dcv = (int16_t)(dc_pred[pidx] << (3 - h.intra_dc_precision));
-                out.coefs.push_back(MP2VG_COEF_PACK(dcv, 0, b, MP2VG_COEF_DC));
+                out.coefs.push_back(MP2VG_COEF_PACK(dcv, 0, b, MP2VG_COEF_DC | MP2VG_COEF_MBX(x)));
                 i = 1;
             } else {
                 // non-intra first coefficient '1s' (mb_decoder.cpp:79-88)
                 uint32_t c = br.peek(2);
                 if (c & 2) {
                     int lvl = (c & 1) ? -1 : 1;
-                    out.coefs.push_back(MP2VG_COEF_PACK(lvl, 0, b, MP2VG_COEF_FIRST1S));
+                    out.coefs.push_back(MP2VG_COEF_PACK(lvl, 0, b, MP2VG_COEF_FIRST1S | MP2VG_COEF_MBX(x)));
                     br.skip(2);
                     i = 1;
                 }
@@ -358,7 +358,7 @@ void parse_slice(const Ctx& C, const PicWork& P, const SliceJob& job, mp2vg_mb_t
                 }
                 i += run;
                 if (i > 63) FAIL(MP2VG_E_BITSTREAM, "coefficient run past position 63");
-                out.coefs.push_back(MP2VG_COEF_PACK(level, i, b, 0));
+                out.coefs.push_back(MP2VG_COEF_PACK(level, i, b, MP2VG_COEF_MBX(x)));
                 i++;
             }
         }

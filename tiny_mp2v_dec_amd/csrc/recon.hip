@@ -287,12 +287,13 @@ constexpr uint32_t kNoTap = 0xFFFFFF00u;
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t slot_rsrc(const uint8_t* base, uint32_t bytes) {
     return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)bytes, 0x00020000);  // gfx9 raw buffer
 }
-template <int NW>
+template <int NW, int ABL = 0>
 __device__ __forceinline__ void load_row(uint32_t (&d)[NW + 1], __amdgpu_buffer_rsrc_t r, uint32_t off) {
     if (NW == 4) {
         const u4v v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0);
         d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
-        d[4] = __builtin_amdgcn_raw_buffer_load_b32(r, (int)(off + 16), 0, 0);
+        // (dev ablation 128: no 17th-pixel dword)
+        d[4] = __builtin_amdgcn_raw_buffer_load_b32(r, (ABL & 128) ? (int)kNoTap : (int)(off + 16), 0, 0);
     } else if (NW == 2) {
         const u3v v = __builtin_amdgcn_raw_buffer_load_b96(r, (int)off, 0, 0);
         d[0] = v.x; d[1] = v.y; d[2] = v.z;
@@ -327,18 +328,22 @@ __device__ __forceinline__ void tap_issue(Tap<NW>& t, bool use, __amdgpu_buffer_
     const int hx = mvx & 1, hy = mvy & 1;
     const bool edge = py + step >= phm;
     t.ctl = (uint32_t)((Xc & 3) | (hx << 2) | (hy << 3) | ((int)use << 4) | ((int)edge << 5) | ((int)field << 6));
+    // dword-aligned row start: byte-exact (unaligned) buffer loads would save two alignbytes per
+    // dword but cost twice the texture-address cycles, a net loss (tools/unaligned_check.hip)
     const uint32_t row = plane_off + (uint32_t)(Xc & ~3);
     const uint32_t o0 = (use && !(ABL & 32)) ? row + (uint32_t)(Y0 * stride) : kNoTap;
     const uint32_t o1 = (use && hy && edge && !(ABL & 32)) ? row + (uint32_t)(Y1 * stride) : kNoTap;
-    load_row<NW>(t.a, ref, o0);
-    load_row<NW>(t.b, ref, o1);
+    load_row<NW, ABL>(t.a, ref, o0);
+    load_row<NW, ABL>(t.b, ref, o1);
 }
 
 // second rows from the next-row lanes (all lanes active: called outside divergent code)
 template <int NW>
 __device__ __forceinline__ void tap_rows(Tap<NW>& t, int lane) {
-    const int src = ((lane + ((t.ctl & 64) ? 8 : 4)) & 63) * 4;
-    const bool edge = t.ctl & 32;
+    // no vertical half-pel: the second row is the lane's own (avg(r, r) == r, no select later)
+    const bool hy = t.ctl & 8;
+    const int src = hy ? ((lane + ((t.ctl & 64) ? 8 : 4)) & 63) * 4 : lane * 4;
+    const bool edge = hy && (t.ctl & 32);
 #pragma unroll
     for (int i = 0; i <= NW; i++) {
         const uint32_t nb = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)t.a[i]);
@@ -347,11 +352,11 @@ __device__ __forceinline__ void tap_rows(Tap<NW>& t, int lane) {
 }
 
 // cascaded half-pel average of one row (mc_sse2.hpp:5-39 == mc_c.hpp:15), branch-free:
-// alignbyte by hx (0 or 1) yields the x+1 pixels or the row itself, and avg(x, x) == x.
+// alignbyte by hx (0 or 1) yields the x+1 pixels or the row itself, and avg(x, x) == x (the
+// second row of a lane without vertical half-pel is its own row, see tap_rows).
 template <int NW>
 __device__ __forceinline__ void tap_finish(const Tap<NW>& t, uint32_t (&p)[NW]) {
     const uint32_t s = t.ctl & 3, hx = (t.ctl >> 2) & 1;
-    const bool hy = t.ctl & 8;
     uint32_t A[NW + 1], C[NW + 1];
 #pragma unroll
     for (int d = 0; d < NW; d++) {
@@ -364,7 +369,7 @@ __device__ __forceinline__ void tap_finish(const Tap<NW>& t, uint32_t (&p)[NW]) 
     for (int d = 0; d < NW; d++) {
         const uint32_t r0 = avg4(A[d], __builtin_amdgcn_alignbyte(A[d + 1], A[d], hx));
         const uint32_t r1 = avg4(C[d], __builtin_amdgcn_alignbyte(C[d + 1], C[d], hx));
-        p[d] = hy ? avg4(r0, r1) : r0;
+        p[d] = avg4(r0, r1);
     }
 }
 
@@ -433,7 +438,7 @@ __device__ __forceinline__ void issue_pass(const LaneRec& L, bool live, int lane
 
 // ---- add/clip + store ----------------------------------------------------------------------
 template <int CF, int J, int NW, int ABL>
-__device__ __forceinline__ void store_pass(uint32_t r0, uint32_t r1, bool live, int lane, const Geo& geo,
+__device__ __forceinline__ void store_pass(uint32_t r0, uint32_t r1, bool live, int lane, const Geo& geo, uint8_t* wsink,
                                            uint8_t* dst_slot, const short* s_res_wave, const uint32_t (&p)[NW]) {
     using F = Fmt<CF>;
     using RL = ResLayout<CF>;
@@ -476,7 +481,7 @@ __device__ __forceinline__ void store_pass(uint32_t r0, uint32_t r1, bool live, 
     const int phm = plane == 0 ? 16 : F::CH;
     uint8_t* dst = dst_slot + gsel(geo.plane_off, plane) +
                    (size_t)((int)(r0 >> 16) * phm + py) * gsel(geo.stride, plane) + (int)(r0 & 0xffff) * pw;
-    dst = live ? dst : geo.sink;  // branch-free: every lane stores (see Tap)
+    dst = live ? dst : wsink;  // branch-free: every lane stores (see Tap)
     if (ABL & 8) {
         asm volatile("" ::"v"(out[0]), "v"(out[1]), "v"(out[2]), "v"(out[3]), "v"(dst));
     } else if (NW == 4) {
@@ -487,10 +492,13 @@ __device__ __forceinline__ void store_pass(uint32_t r0, uint32_t r1, bool live, 
 }
 
 // ---- one slice ------------------------------------------------------------------------------
+constexpr int BLKS = 72;
 template <int CF>
 struct Lds {
     static constexpr int MAXS = G * Fmt<CF>::NB;  // coded-block slots per group
-    short blk[WAVES][MAXS][64];                  // coef raster -> pass-1 out
+    // coef raster -> pass-1 out; slots 144 B apart (BLKS shorts): the transposed pass-1 writes of
+    // the 8 slots in a 32-lane half then hit distinct banks (128 B apart: 8-way conflicts)
+    short blk[WAVES][MAXS][BLKS];
     short res[WAVES][G * ResLayout<CF>::SIZE];
     uint8_t map[WAVES][MAXS];                    // slot -> k*16 + b
     uint8_t W[4][64];
@@ -501,6 +509,9 @@ struct SliceCtx {
     const uint32_t* mbrec;
     const uint32_t* coefs;
     uint8_t* dst_slot;
+    // this wave's own 64-B sink line (dummy and dead-lane stores): stores of many waves to one
+    // address serialize in one L2 channel, and a wave's first loop-head wait covers its own
+    uint8_t* wsink;
     __amdgpu_buffer_rsrc_t ref_fwd, ref_bwd;
     uint32_t mb_begin, mb_end;
 };
@@ -589,7 +600,10 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, Lds
     Tap<NWC> t1f, t1b;  // chroma rows (4:2:0: Cb + Cr; else Cb)
     Tap<NWC> t2f, t2b;  // Cr rows (4:2:2 / 4:4:4)
     Group S;
-    uint32_t gr0, gr1, rvN, cw0, cw1;
+    // coefficient words prefetched one group ahead, 64 per register: intra groups (I pictures) carry
+    // ~180 words, and a word past the prefetch is a synchronous load (a full memory latency)
+    constexpr int NCW = MCM == 0 ? 4 : 2;
+    uint32_t gr0, gr1, rvN, cw[NCW];
     bool glive;
     {
         const uint32_t rv = rec_load(c.mbrec, g, mb_last, lane);
@@ -602,8 +616,8 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, Lds
         gr1 = R.r1;
         __builtin_amdgcn_sched_barrier(0);
         rvN = rec_load(c.mbrec, g + STEP < mb_end ? g + STEP : g, mb_last, lane);
-        cw0 = c.coefs[S.coef0 + lane];
-        cw1 = c.coefs[S.coef0 + 64 + lane];
+#pragma unroll
+        for (int j = 0; j < NCW; j++) cw[j] = c.coefs[S.coef0 + 64 * j + lane];
         __builtin_amdgcn_sched_barrier(0);
         if (MCM) {
             issue_pass<CF, MCM, 1, NWC, ABL>(R, glive, lane, geo, c.ref_fwd, c.ref_bwd, t1f, t1b);
@@ -615,7 +629,7 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, Lds
         // vmcnt state at the loop head does not degrade to vmcnt(0)
         if (!(ABL & 8)) {
 #pragma unroll
-            for (int j = 0; j < Passes<CF>::N; j++) ((uint32_t*)geo.sink)[j * 64] = 0u;
+            for (int j = 0; j < Passes<CF>::N; j++) ((uint32_t*)c.wsink)[j * 4] = 0u;  // 16 B apart: not merged
         }
     }
 
@@ -659,16 +673,17 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, Lds
                 L.map[wave][(int)pick8(S.sb8, k) + __builtin_popcount(cbpk & ((1u << bb) - 1))] = (uint8_t)(k * 16 + bb);
         }
         if (!(ABL & 4)) {
-            // words 0..127 from the registers loaded one group ahead; more (rare) loaded here
-            if (lane < S.ncoef) dequant_word<CF>(L, wave, S, cw0, lane);
-            if (64 + lane < S.ncoef) dequant_word<CF>(L, wave, S, cw1, 64 + lane);
-            for (int w_idx = 128 + lane; w_idx < S.ncoef; w_idx += 64)
+            // words 0..64*NCW-1 from the registers loaded one group ahead; more (rare) loaded here
+#pragma unroll
+            for (int j = 0; j < NCW; j++)
+                if (64 * j + lane < S.ncoef) dequant_word<CF>(L, wave, S, cw[j], 64 * j + lane);
+            for (int w_idx = 64 * NCW + lane; w_idx < S.ncoef; w_idx += 64)
                 dequant_word<CF>(L, wave, S, c.coefs[S.coef0 + w_idx], w_idx);
         }
-        // first 128 coefficient words of g+1 (the words of g are consumed)
+        // first 64*NCW coefficient words of g+1 (the words of g are consumed)
         __builtin_amdgcn_sched_barrier(0);
-        cw0 = c.coefs[SN.coef0 + lane];
-        cw1 = c.coefs[SN.coef0 + 64 + lane];
+#pragma unroll
+        for (int j = 0; j < NCW; j++) cw[j] = c.coefs[SN.coef0 + 64 * j + lane];
         __builtin_amdgcn_sched_barrier(0);
         wave_sync();
 
@@ -734,9 +749,9 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, Lds
 
         stamp<ABL>(st, 4);
         // ---- E. prediction + residual, one row store per lane ----
-        store_pass<CF, 0, 4, ABL>(gr0, gr1, glive, lane, geo, c.dst_slot, L.res[wave], p0);
-        store_pass<CF, 1, NWC, ABL>(gr0, gr1, glive, lane, geo, c.dst_slot, L.res[wave], p1);
-        if (CF != 1) store_pass<CF, 2, NWC, ABL>(gr0, gr1, glive, lane, geo, c.dst_slot, L.res[wave], p2);
+        store_pass<CF, 0, 4, ABL>(gr0, gr1, glive, lane, geo, c.wsink, c.dst_slot, L.res[wave], p0);
+        store_pass<CF, 1, NWC, ABL>(gr0, gr1, glive, lane, geo, c.wsink, c.dst_slot, L.res[wave], p1);
+        if (CF != 1) store_pass<CF, 2, NWC, ABL>(gr0, gr1, glive, lane, geo, c.wsink, c.dst_slot, L.res[wave], p2);
         wave_sync();
 
         stamp<ABL>(st, 5);
@@ -775,13 +790,14 @@ __global__ __launch_bounds__(256) void recon_kernel(const mp2vg_picture_t* __res
         ((uint32_t*)L.W)[tid] = ((const uint32_t*)pic->W)[tid];
         L.scan[tid] = c_scan_raster[alt][tid];
     }
-    for (int i = lane; i < Lds<CF>::MAXS * 64 / 2; i += 64) ((uint32_t*)L.blk[wave])[i] = 0;
+    for (int i = lane; i < Lds<CF>::MAXS * BLKS / 2; i += 64) ((uint32_t*)L.blk[wave])[i] = 0;
     __syncthreads();
 
     SliceCtx c;
     c.mbrec = mbrec;
     c.coefs = coefs;
     c.dst_slot = pool + (uint64_t)pic->dst_slot * geo.slot_bytes;
+    c.wsink = geo.sink + 2048 + ((b * WAVES + wave) & 1023) * 64;
     c.ref_fwd = slot_rsrc(pool + (uint64_t)(pic->fwd_slot < 0 ? pic->dst_slot : pic->fwd_slot) * geo.slot_bytes,
                           (uint32_t)geo.slot_bytes);
     c.ref_bwd = slot_rsrc(pool + (uint64_t)(pic->bwd_slot < 0 ? pic->dst_slot : pic->bwd_slot) * geo.slot_bytes,
@@ -850,7 +866,7 @@ hipError_t launch_recon(int cf, int mcm, const KArgs& a, hipStream_t stream) {
     g.sink = a.sink;
     g.slot_bytes = a.slot_bytes;
     for (int i = 0; i < 3; i++) {
-        g.plane_off[i] = a.plane_off[i];
+        g.plane_off[i] = (uint32_t)a.plane_off[i];
         g.stride[i] = a.stride[i];
         g.ph[i] = a.ph[i];
     }
@@ -868,6 +884,7 @@ hipError_t launch_recon(int cf, int mcm, const KArgs& a, hipStream_t stream) {
         case 32: return launch_mcm<1, 32>(mcm, a, g, stream);
         case 64: return launch_mcm<1, 64>(mcm, a, g, stream);
         case 96: return launch_mcm<1, 96>(mcm, a, g, stream);
+        case 128: return launch_mcm<1, 128>(mcm, a, g, stream);
         default: return hipErrorInvalidValue;
         }
     }

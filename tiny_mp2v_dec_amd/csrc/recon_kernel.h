@@ -42,7 +42,7 @@ struct Launch {
 struct Geo {
     uint8_t* sink;  // 16+ writable, readable bytes outside every slot: dummy loads and stores
     uint64_t slot_bytes;
-    uint64_t plane_off[3];
+    uint32_t plane_off[3];  // plane offsets inside a slot (a slot is < 4 GiB)
     int32_t stride[3];
     int32_t ph[3];
 };

@@ -34,10 +34,11 @@ using namespace mp2vg;
         }                                                                                  \
     } while (0)
 
-static constexpr size_t kPoolPad = 4096;       // slack after the last slot: clamped row over-reads, and the
-                                               // kernel's dummy load / store sink at +2048 (kSinkOff)
+static constexpr size_t kPoolPad = 4096 + 65536;  // slack after the last slot: clamped row over-reads, the
+                                                  // kernel's dummy load / store sink at +2048 (kSinkOff) and,
+                                                  // from +4096, one 64-B sink line per wave (1024 lines)
 static constexpr size_t kSinkOff = 2048;
-static constexpr size_t kCoefPad = 128;        // the kernel prefetches 128 coefficient words per MB group
+static constexpr size_t kCoefPad = 256;        // the kernel prefetches up to 256 coefficient words per MB group
 static constexpr size_t kStageBytes = 32u << 20;
 static constexpr size_t kMbPad = 16;  // >= the kernel's MB group size
 
@@ -170,7 +171,7 @@ extern "C" int mp2vg_reserve_slots(mp2vg_ctx_t* c, int32_t nslots) {
 
 // Validate the batch so no kernel access can leave its buffers, and compute dependency levels.
 static int plan_batch(mp2vg_ctx_t* c, const mp2vg_picture_t* pics, int32_t npics, const mp2vg_mb_t* mbs,
-                      uint64_t nmbs, uint64_t ncoefs, std::vector<SliceDesc>& slices,
+                      uint64_t nmbs, const uint32_t* coefs, uint64_t ncoefs, std::vector<SliceDesc>& slices,
                       std::vector<Launch>& launches) {
     const int mbw = c->cfg.width / 16, mbh = c->cfg.height / 16;
     const int nb = c->g.nblocks;
@@ -202,6 +203,14 @@ static int plan_batch(mp2vg_ctx_t* c, const mp2vg_picture_t* pics, int32_t npics
             if ((uint64_t)m.coef_off + m.ncoef > ncoefs) {
                 set_error("MB coefficient range outside the batch");
                 return MP2VG_E_INVALID;
+            }
+            // the kernel takes a word's MB (inside its 8-MB group) from bits 28-30
+            const uint32_t tag = MP2VG_COEF_MBX(m.x);
+            for (uint32_t j = 0; j < m.ncoef; j++) {
+                if ((coefs[m.coef_off + j] & 0xF0000000u) != tag) {
+                    set_error("coefficient word bits 28-31 are not the MB column mod 8");
+                    return MP2VG_E_INVALID;
+                }
             }
             // the kernel streams the coefficient words of consecutive MBs of a row as one range
             if (k % mbw != 0) {
@@ -273,7 +282,7 @@ extern "C" int mp2vg_batch_upload(mp2vg_ctx_t* c, const mp2vg_picture_t* pics, i
     c->batch_ready = false;
     std::vector<SliceDesc> slices;
     std::vector<Launch> lb;
-    int rc = plan_batch(c, pics, npics, mbs, nmbs, ncoefs, slices, lb);
+    int rc = plan_batch(c, pics, npics, mbs, nmbs, coefs, ncoefs, slices, lb);
     if (rc != MP2VG_OK) return rc;
     HIPCHK(hipStreamSynchronize(c->stream));
     if ((rc = grow(c->d_pics, c->cap_pics, (size_t)npics)) != MP2VG_OK) return rc;

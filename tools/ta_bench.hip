@@ -27,6 +27,7 @@ __global__ __launch_bounds__(256) void kern(const uint8_t* __restrict__ buf, uin
         else if (P == 2) off = row * 2048u + lane * 16;
         else if (P == 4) off = row * 2048u + lane * 4;
         else if (P == 5 || P == 6 || P == 9) off = (lane < 16) ? ((row + lane) & 2047u) * 2048u + 8 : 64;
+        else if (P == 10) off = ((row + (lane & 15)) & 2047u) * 2048u + (lane >> 4) * 16;  // 16 rows, MB k = lane >> 4
         else off = ((row + (lane >> 1)) & 2047u) * 2048u + (lane & 1) * 16;  // P == 8
         if (P == 3 || P == 4 || P == 9) {
             acc += *(const uint32_t*)(buf + off);
@@ -83,5 +84,6 @@ int main() {
     run<5>("x4  16 rows + 48 lanes same addr", buf, out);
     run<6>("x4  16 rows, 48 lanes masked", buf, out);
     run<9>("x1  16 rows + 48 lanes same addr", buf, out);
+    run<10>("x4  16 rows x 4 lanes, lanes 16 apart", buf, out);
     return 0;
 }

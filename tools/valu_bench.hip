@@ -32,6 +32,8 @@ __global__ __launch_bounds__(256) void kern(uint32_t* out, uint32_t seed) {
             if (OP == 10) v[i] = v[i] + v[(i + 3) & 7];                                 // v_add_u32 (no folding)
             if (OP == 11) v[i] = v[i] ^ v[(i + 3) & 7];                                 // v_xor_b32
             if (OP == 12) v[i] = __builtin_bit_cast(uint32_t, __builtin_fmaf(__builtin_bit_cast(float, v[i]), 1.0001f, __builtin_bit_cast(float, k)));  // v_fma_f32
+            if (OP == 14) v[i] = __builtin_amdgcn_mov_dpp(v[i], 0x101, 0xf, 0xf, false);      // v_mov_b32_dpp row_shl:1
+            if (OP == 15) v[i] = __builtin_amdgcn_mov_dpp(v[i], 0x153, 0xf, 0xf, false) ^ v[(i + 1) & 7];  // dpp newbcast + xor
             if (OP == 13) v[i] = __builtin_amdgcn_perm(v[i], v[(i + 3) & 7], 0x05040100u);  // v_perm, 2 VGPR operands
         }
     }
@@ -76,5 +78,7 @@ int main() {
     run<11>("v_xor_b32 (cross-chain)", out);
     run<12>("v_fma_f32", out);
     run<13>("v_perm_b32 (2 VGPR srcs)", out);
+    run<14>("v_mov_b32_dpp row_shl:1", out);
+    run<15>("dpp row_newbcast + v_xor", out);
     return 0;
 }
