@@ -138,7 +138,9 @@ def main():
         dist.barrier()
 
     width, height, cf, gparams, desc = CONFIGS[args.config]
-    gops = args.gops if args.config != "c5" else args.gops * 12 // max(1, gparams["gop_n"])
+    # c5 is I-only: one picture per "GOP", so --gops is its frame count (~60 frames; at
+    # 768 frames its elementary stream would pass the 2 GB `int len` of the reference decode() API)
+    gops = args.gops
     es = R.generate_es(width=width, height=height, chroma_format=cf, n_gops=gops, seed=1729 + rank, **gparams)
     parsed = R.Parsed(es, width, height, cf, threads=min(8, os.cpu_count() or 1))
     alg_bytes, parts = algorithmic_bytes(parsed)

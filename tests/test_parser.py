@@ -146,3 +146,20 @@ def test_generated_streams_parse(seed):
                      f_code=int(rng.integers(1, 6)), big_level_permille=100, escape_permille=200)
     p = _parse(es, cf=cf)
     assert p.npics >= 2
+
+
+def test_copy_out_matches_bytes_and_dtype():
+    """records._copy_out (numpy view over a library pointer) replaces ctypes.string_at, whose C int
+    size went negative past 2 GiB and truncated large batches' coefficient arrays."""
+    import ctypes
+
+    import numpy as np
+
+    from tiny_mp2v_dec_amd import records as R
+
+    src = ((np.arange(1000, dtype=np.uint64) * 2654435761) % (1 << 32)).astype(np.uint32)
+    ptr = ctypes.c_void_p(src.ctypes.data)
+    out = R._copy_out(ptr, src.nbytes, np.uint32)
+    assert out.dtype == np.uint32 and np.array_equal(out, src)
+    assert out.ctypes.data != src.ctypes.data  # a copy, not a view of library memory
+    assert R._copy_out(ptr, 0, np.uint32).size == 0

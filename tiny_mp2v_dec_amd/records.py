@@ -20,13 +20,22 @@ def gen_params(**kw):
     return p
 
 
+def _copy_out(ptr, nbytes, dtype=np.uint8):
+    """Copy nbytes at a library-owned pointer into a new array.  ctypes.string_at takes a C int size,
+    which goes negative (or wraps) past 2 GiB; a numpy view over the pointer has no such limit."""
+    if not nbytes:
+        return np.zeros(0, dtype)
+    raw = np.ctypeslib.as_array(ctypes.cast(ptr, ctypes.POINTER(ctypes.c_uint8)), shape=(nbytes,))
+    return raw.view(dtype).copy()
+
+
 def generate_es(**kw):
     """Write a synthetic elementary stream of the reference's decodable subset (bytes)."""
     p = gen_params(**kw)
     ptr, n = ctypes.c_void_p(), ctypes.c_uint64()
     check(lib().mp2vg_generate_es(ctypes.byref(p), ctypes.byref(ptr), ctypes.byref(n)), "generate_es")
     try:
-        return ctypes.string_at(ptr, n.value)
+        return _copy_out(ptr, n.value).tobytes()
     finally:
         lib().mp2vg_free(ptr)
 
@@ -45,10 +54,9 @@ class Parsed:
             npics, nmbs, ncoefs = ctypes.c_int32(), ctypes.c_uint64(), ctypes.c_uint64()
             lib().mp2vg_parsed_counts(h, ctypes.byref(npics), ctypes.byref(nmbs), ctypes.byref(ncoefs))
             n, m, c = npics.value, nmbs.value, ncoefs.value
-            self.pics = np.frombuffer(ctypes.string_at(lib().mp2vg_parsed_pictures(h), n * 288), PIC_DTYPE).copy()
-            self.mbs = np.frombuffer(ctypes.string_at(lib().mp2vg_parsed_mbs(h), m * 32), MB_DTYPE).copy()
-            self.coefs = (np.frombuffer(ctypes.string_at(lib().mp2vg_parsed_coefs(h), c * 4), np.uint32).copy()
-                          if c else np.zeros(0, np.uint32))
+            self.pics = _copy_out(lib().mp2vg_parsed_pictures(h), n * 288, PIC_DTYPE)
+            self.mbs = _copy_out(lib().mp2vg_parsed_mbs(h), m * 32, MB_DTYPE)
+            self.coefs = _copy_out(lib().mp2vg_parsed_coefs(h), c * 4, np.uint32)
             order = (ctypes.c_int32 * max(n, 1))()
             lib().mp2vg_parsed_display_order(h, order, n)
             self.display = np.array(order[:n], dtype=np.int32)
