@@ -84,7 +84,8 @@ typedef struct mp2vg_mb {
  * bit 26 FIRST1S: non-intra first coefficient coded with the B.14 '1s' code — dequantised as
  * (3*W[0]*qs)>>5 without the +-2047 clamp (mb_decoder.cpp:79-88), bit 27 DC: intra DC value,
  * excluded from the mismatch parity (mb_decoder.cpp:76,160), bits 28-30: the MB's column x
- * mod 8 (its index in the kernel's 8-MB group; mp2vg_batch_upload validates it), bit 31: 0.
+ * mod 8 (the kernel finds a word's MB in its 4-MB group from it; mp2vg_batch_upload
+ * validates it), bit 31: 0.
  * Words of one MB are grouped by block, blocks in bitstream order.                           */
 #define MP2VG_COEF_LEVEL(w) ((int16_t)((w) & 0xffffu))
 #define MP2VG_COEF_POS(w) (((w) >> 16) & 63u)

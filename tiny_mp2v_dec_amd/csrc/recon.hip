@@ -201,7 +201,7 @@ struct Group {
     uint32_t qs8;           // byte k: quantiser_scale
     uint32_t sb8;           // byte k: first coded-block slot of MB k in the group
     uint32_t cbp01, cbp23;  // 16-bit coded_block_pattern of MBs 0,1 / 2,3 (0 if absent)
-    uint32_t crel1, crel2, crel3;  // first coefficient word of MBs 1..3, relative to coef0
+    uint32_t x0;            // column of MB 0 mod 8: a coefficient word's MB is ((w >> 28) - x0) & 7
     int nslots, ncoef;
     uint32_t coef0;
 };
@@ -220,9 +220,9 @@ __device__ __forceinline__ void group_mb(Group& S, uint32_t rv, int ng, int& sb,
     S.qs8 |= (r2 & 0xff) << (8 * K);
     S.sb8 |= (uint32_t)sb << (8 * K);
     if (K == 0) S.cbp01 = cbpk;
-    if (K == 1) S.cbp01 |= cbpk << 16, S.crel1 = (uint32_t)cr;
-    if (K == 2) S.cbp23 = cbpk, S.crel2 = (uint32_t)cr;
-    if (K == 3) S.cbp23 |= cbpk << 16, S.crel3 = (uint32_t)cr;
+    if (K == 1) S.cbp01 |= cbpk << 16;
+    if (K == 2) S.cbp23 = cbpk;
+    if (K == 3) S.cbp23 |= cbpk << 16;
     sb += __builtin_popcount(cbpk);
     cr += live ? (int)(r2 >> 16) : 0;
 }
@@ -239,6 +239,7 @@ __device__ __forceinline__ Group group_state(uint32_t rv, int ng) {
     S.nslots = sb;
     S.ncoef = cr;
     S.coef0 = rec_uni<3, 0>(rv);
+    S.x0 = rec_uni<0, 0>(rv) & 7u;
     return S;
 }
 
@@ -517,11 +518,11 @@ struct SliceCtx {
 };
 
 // dequant of one coefficient word (parse_block, mb_decoder.cpp:74-155) into its coded-block
-// slot: lane = word, MB k from the group's coefficient offsets
+// slot: lane = word, MB k from the word's MB-column bits
 template <int CF>
-__device__ __forceinline__ void dequant_word(Lds<CF>& L, int wave, const Group& S, uint32_t w, int w_idx) {
+__device__ __forceinline__ void dequant_word(Lds<CF>& L, int wave, const Group& S, uint32_t w) {
     constexpr int NB = Fmt<CF>::NB;
-    const int k = (w_idx >= (int)S.crel1) + (w_idx >= (int)S.crel2) + (w_idx >= (int)S.crel3);
+    const int k = (int)(((w >> 28) - S.x0) & 7u);  // MB column bits (include/mp2vg.h), checked on upload
     const uint32_t cbpk = pick16(S.cbp01, S.cbp23, k);
     const int bb = (w >> 22) & 15;
     if (bb >= NB || !(cbpk & (1u << bb))) return;  // host validation rejects these
@@ -676,9 +677,9 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, Lds
             // words 0..64*NCW-1 from the registers loaded one group ahead; more (rare) loaded here
 #pragma unroll
             for (int j = 0; j < NCW; j++)
-                if (64 * j + lane < S.ncoef) dequant_word<CF>(L, wave, S, cw[j], 64 * j + lane);
+                if (64 * j + lane < S.ncoef) dequant_word<CF>(L, wave, S, cw[j]);
             for (int w_idx = 64 * NCW + lane; w_idx < S.ncoef; w_idx += 64)
-                dequant_word<CF>(L, wave, S, c.coefs[S.coef0 + w_idx], w_idx);
+                dequant_word<CF>(L, wave, S, c.coefs[S.coef0 + w_idx]);
         }
         // first 64*NCW coefficient words of g+1 (the words of g are consumed)
         __builtin_amdgcn_sched_barrier(0);
