@@ -161,7 +161,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         ctx.decode()
-        kernel_ms.append(ctx.launch_times_ms())  # HIP events on each launch's stream
+        kernel_ms.append(ctx.launch_times_ms())  # HIP events around each launch
         batch_ms.append(ctx.batch_time_ms())  # first launch start -> last launch end
     ctx.synchronize()
     barrier()
@@ -186,8 +186,8 @@ def main():
     frames_total = parsed.npics * world * args.steps
     ms_per_step = elapsed * 1000.0 / args.steps
     per_launch = [x for step in kernel_ms for x in step]
-    # launches of one dependency level overlap on two streams: the kernel time of a step is the
-    # device span of the batch, not the sum of the launches
+    # the kernel time of a step is the device span of the batch (HIP events on the launch stream,
+    # first launch start -> last launch end), which includes the gaps between its launches
     kernel_step_ms = float(np.mean(batch_ms))
     achieved = alg_bytes / (kernel_step_ms / 1000.0) / 1e9
     result = {
