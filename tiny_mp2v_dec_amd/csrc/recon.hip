@@ -805,7 +805,17 @@ __global__ __launch_bounds__(256) void recon_kernel(const mp2vg_picture_t* __res
                           (uint32_t)geo.slot_bytes);
     c.mb_begin = sd.mb_begin;
     c.mb_end = sd.mb_begin + sd.mb_count;
-    run_slice<CF, (ABL & 2) ? 0 : MCM, ABL>(c, geo, L, lane, wave);
+    if (MCM < 3) {
+        run_slice<CF, (ABL & 2) ? 0 : MCM, ABL>(c, geo, L, lane, wave);
+    } else {  // mixed level: the picture type picks the specialised loop (uniform per workgroup)
+        const int pct = pic->picture_coding_type;
+        if (pct == 3)
+            run_slice<CF, (ABL & 2) ? 0 : 2, ABL>(c, geo, L, lane, wave);
+        else if (pct == 2)
+            run_slice<CF, (ABL & 2) ? 0 : 1, ABL>(c, geo, L, lane, wave);
+        else
+            run_slice<CF, 0, ABL>(c, geo, L, lane, wave);
+    }
 }
 // Order-independent 64-bit digest of a slot's visible planes:
 //   sum over visible dwords d at (row_id, byte x) of mix64((row_id << 32) | x) ^ d   (mod 2^64)
@@ -857,6 +867,7 @@ static hipError_t launch_mcm(int mcm, const KArgs& a, const Geo& g, hipStream_t 
     case 0: launch_one<CF, 0, ABL>(a, g, stream); break;
     case 1: launch_one<CF, 1, ABL>(a, g, stream); break;
     case 2: launch_one<CF, 2, ABL>(a, g, stream); break;
+    case 3: launch_one<CF, 3, ABL>(a, g, stream); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

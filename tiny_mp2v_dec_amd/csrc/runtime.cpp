@@ -251,24 +251,29 @@ static int plan_batch(mp2vg_ctx_t* c, const mp2vg_picture_t* pics, int32_t npics
         max_read[P.dst_slot] = -1;
         maxlevel = std::max(maxlevel, lv);
     }
-    // one launch per (level, motion-compensation mode): I pictures (none), P (forward only),
-    // B (both directions) each run a kernel specialised -- and register-allocated -- for it
-    std::vector<std::vector<int>> bylevel(3 * (maxlevel + 1));
-    for (int p = 0; p < npics; p++) {
-        const int pct = pics[p].picture_coding_type;
-        bylevel[3 * level[p] + (pct == 1 ? 0 : (pct == 2 ? 1 : 2))].push_back(p);
-    }
+    // one launch per dependency level.  A level of one picture type runs the kernel specialised --
+    // and register-allocated -- for its motion-compensation mode: I (none), P (forward only), B
+    // (both directions).  A level that mixes types (B pictures next to the following P anchor)
+    // runs the mixed kernel, which picks the mode per workgroup from the picture type: one launch
+    // tail per level instead of one per type.  Pictures stay in decode order, so every XCD's
+    // contiguous share of the slices holds the same mix of P and B work.
+    std::vector<std::vector<int>> bylevel(maxlevel + 1);
+    for (int p = 0; p < npics; p++) bylevel[level[p]].push_back(p);
     slices.clear();
     launches.clear();
     for (size_t q = 0; q < bylevel.size(); q++) {
         if (bylevel[q].empty()) continue;
         Launch l;
         l.begin = (uint32_t)slices.size();
-        for (int p : bylevel[q])
+        int types = 0;
+        for (int p : bylevel[q]) {
+            const int pct = pics[p].picture_coding_type;
+            types |= 1 << (pct == 1 ? 0 : (pct == 2 ? 1 : 2));
             for (int r = 0; r < mbh; r++) slices.push_back({(uint32_t)p, pics[p].mb_first + (uint32_t)(r * mbw), (uint32_t)mbw, 0});
+        }
         l.end = (uint32_t)slices.size();
-        l.mcm = (int)(q % 3);
-        l.level = (int)(q / 3);
+        l.mcm = types == 1 ? 0 : (types == 2 ? 1 : (types == 4 ? 2 : 3));
+        l.level = (int)q;
         launches.push_back(l);
     }
     return MP2VG_OK;
