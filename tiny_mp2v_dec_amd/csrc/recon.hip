@@ -678,8 +678,20 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, Lds
 #pragma unroll
             for (int j = 0; j < NCW; j++)
                 if (64 * j + lane < S.ncoef) dequant_word<CF>(L, wave, S, cw[j]);
-            for (int w_idx = 64 * NCW + lane; w_idx < S.ncoef; w_idx += 64)
-                dequant_word<CF>(L, wave, S, c.coefs[S.coef0 + w_idx]);
+            // words past the prefetch: XW loads per lane in flight per round trip, not one (a 4:4:4
+            // intra group carries ~1,400 words)
+            constexpr int XW = MCM == 0 ? 8 : 2;
+            for (int base = 64 * NCW; base < S.ncoef; base += 64 * XW) {
+                uint32_t xw[XW];
+#pragma unroll
+                for (int j = 0; j < XW; j++) {
+                    const int wi = base + 64 * j + lane;
+                    xw[j] = wi < S.ncoef ? c.coefs[S.coef0 + wi] : 0u;
+                }
+#pragma unroll
+                for (int j = 0; j < XW; j++)
+                    if (base + 64 * j + lane < S.ncoef) dequant_word<CF>(L, wave, S, xw[j]);
+            }
         }
         // first 64*NCW coefficient words of g+1 (the words of g are consumed)
         __builtin_amdgcn_sched_barrier(0);
