@@ -335,7 +335,8 @@ __device__ __forceinline__ void tap_issue(Tap<NW>& t, bool use, __amdgpu_buffer_
     const uint32_t o0 = (use && !(ABL & 32)) ? row + (uint32_t)(Y0 * stride) : kNoTap;
     const uint32_t o1 = (use && hy && edge && !(ABL & 32)) ? row + (uint32_t)(Y1 * stride) : kNoTap;
     load_row<NW, ABL>(t.a, ref, o0);
-    load_row<NW, ABL>(t.b, ref, o1);
+    if (!(ABL & 512)) load_row<NW, ABL>(t.b, ref, o1);  // (dev ablation 512: no edge-row loads)
+    else for (int i = 0; i <= NW; i++) t.b[i] = 0;
 }
 
 // second rows from the next-row lanes (all lanes active: called outside divergent code)
@@ -894,8 +895,10 @@ hipError_t launch_recon(int cf, int mcm, const KArgs& a, hipStream_t stream) {
         g.stride[i] = a.stride[i];
         g.ph[i] = a.ph[i];
     }
-    // development-only ablation switch (MP2VG_ABLATE, 4:2:0 only): 1 no IDCT, 2 no MC loads,
-    // 4 no dequant, 8 no stores.  Outputs are wrong under it; never set in tests or the bench.
+    // development-only ablation switch (MP2VG_ABLATE, 4:2:0 only): 1 no IDCT, 2 no MC, 4 no
+    // dequant, 8 no stores, 16 stage stamps (tools/stamps.py), 32 MC loads out of range (no address
+    // math), 64 no prediction arithmetic, 128 no 17th-pixel dwords, 512 no edge-row loads.
+    // Outputs are wrong under it (except 16); never set in tests or the bench.
     static const int ablate = getenv("MP2VG_ABLATE") ? atoi(getenv("MP2VG_ABLATE")) : 0;
     if (cf == 1 && ablate) {
         switch (ablate) {
@@ -909,6 +912,7 @@ hipError_t launch_recon(int cf, int mcm, const KArgs& a, hipStream_t stream) {
         case 64: return launch_mcm<1, 64>(mcm, a, g, stream);
         case 96: return launch_mcm<1, 96>(mcm, a, g, stream);
         case 128: return launch_mcm<1, 128>(mcm, a, g, stream);
+        case 512: return launch_mcm<1, 512>(mcm, a, g, stream);
         default: return hipErrorInvalidValue;
         }
     }
