@@ -30,9 +30,50 @@ using namespace mp2vg;
 namespace {
 constexpr int kChunk = 16;  // pictures per device batch
 
+// Host frames live in pinned memory, in the device slot layout (= the reference frame_c layout),
+// so a decoded slot comes back with one contiguous DMA copy.  They are recycled after the render
+// callback returns (a frame is valid only during the callback, reference threads.cpp:75-80).
 struct HostFrame {
-    std::vector<uint8_t> data;
+    uint8_t* data = nullptr;
     mp2vg_frame_t f;
+};
+
+class FramePool {
+  public:
+    explicit FramePool(size_t bytes) : bytes_(bytes) {}
+    ~FramePool() {
+        for (HostFrame* f : all_) {
+            hipHostFree(f->data);
+            delete f;
+        }
+    }
+    HostFrame* get() {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            if (!free_.empty()) {
+                HostFrame* f = free_.back();
+                free_.pop_back();
+                return f;
+            }
+        }
+        auto* f = new HostFrame();
+        if (hipHostMalloc((void**)&f->data, bytes_, hipHostMallocDefault) != hipSuccess) {
+            delete f;
+            return nullptr;
+        }
+        std::lock_guard<std::mutex> lk(mu_);
+        all_.push_back(f);
+        return f;
+    }
+    void put(HostFrame* f) {
+        std::lock_guard<std::mutex> lk(mu_);
+        free_.push_back(f);
+    }
+
+  private:
+    size_t bytes_;
+    std::mutex mu_;
+    std::vector<HostFrame*> all_, free_;
 };
 }  // namespace
 
@@ -75,7 +116,10 @@ extern "C" int mp2vg_decoder_destroy(mp2vg_decoder_t* d) {
 extern "C" int mp2vg_decoder_decode(mp2vg_decoder_t* d, const uint8_t* buf, uint64_t len) {
     if (!d || !buf) return MP2VG_E_INVALID;
     mp2vg_parsed_t* parsed = nullptr;
+    double t0 = now_ms(), tc;
+    double t_up = 0, t_dec = 0, t_down = 0;
     int rc = mp2vg_parse_es(buf, len, &d->cfg, &parsed);
+    t0 = trace_phase("dropin: parse", t0);
     if (rc != MP2VG_OK) return rc;
     std::unique_ptr<mp2vg_parsed_t, void (*)(mp2vg_parsed_t*)> guard(parsed, mp2vg_parsed_free);
     int32_t npics = 0;
@@ -97,26 +141,31 @@ extern "C" int mp2vg_decoder_decode(mp2vg_decoder_t* d, const uint8_t* buf, uint
     // render thread (decoder.cpp:403, :346-379)
     std::mutex mu;
     std::condition_variable cv;
-    std::deque<std::unique_ptr<HostFrame>> q;
+    std::deque<HostFrame*> q;
     bool done = false;
+    FramePool pool(d->g.slot_bytes);
+    hipStream_t dl = nullptr;
+    if (hipStreamCreateWithFlags(&dl, hipStreamNonBlocking) != hipSuccess) return MP2VG_E_HIP;
+    std::unique_ptr<void, void (*)(void*)> dl_guard(dl, [](void* s) { hipStreamDestroy((hipStream_t)s); });
     std::thread render([&]() {
         for (;;) {
-            std::unique_ptr<HostFrame> f;
+            HostFrame* f;
             {
                 std::unique_lock<std::mutex> lk(mu);
                 cv.wait(lk, [&] { return done || !q.empty(); });
                 if (q.empty()) return;
-                f = std::move(q.front());
+                f = q.front();
                 q.pop_front();
             }
             d->fn(d->user, &f->f);
+            pool.put(f);
         }
     });
 
     std::vector<int> slot_of(npics, -1);
     std::vector<int> free_slots;
     for (int s = d->nslots - 1; s >= 0; s--) free_slots.push_back(s);
-    std::map<int, std::unique_ptr<HostFrame>> ready;  // decode index -> downloaded frame
+    std::map<int, HostFrame*> ready;  // decode index -> downloaded frame
     size_t next_display = 0;
     std::vector<mp2vg_picture_t> cp;
     std::vector<mp2vg_mb_t> cm;
@@ -157,30 +206,39 @@ extern "C" int mp2vg_decoder_decode(mp2vg_decoder_t* d, const uint8_t* buf, uint
         }
         cm.assign(mbs + mb0, mbs + mb1);
         for (auto& m : cm) m.coef_off -= (uint32_t)c0;
+        tc = now_ms();
         rc = mp2vg_batch_upload(d->ctx, cp.data(), (int32_t)cp.size(), cm.data(), cm.size(), coefs + c0, c1 - c0);
+        t_up += now_ms() - tc;
+        tc = now_ms();
         if (rc == MP2VG_OK) rc = mp2vg_batch_decode(d->ctx);
         if (rc == MP2VG_OK) rc = mp2vg_synchronize(d->ctx);
+        t_dec += now_ms() - tc;
+        tc = now_ms();
         if (rc != MP2VG_OK) return finish(rc);
-        // download into frame_c-layout host frames
+        // download into frame_c-layout host frames: one DMA per slot, one wait per chunk
         for (int p = s; p < e; p++) {
-            auto hf = std::make_unique<HostFrame>();
-            hf->data.resize(d->g.slot_bytes);
-            uint8_t* planes[3];
-            int32_t strides[3];
+            HostFrame* hf = pool.get();
+            if (!hf) return finish(MP2VG_E_NOMEM);
             for (int i = 0; i < 3; i++) {
-                planes[i] = hf->data.data() + d->g.plane_off[i];
-                strides[i] = d->g.stride[i];
-                hf->f.planes[i] = planes[i];
+                hf->f.planes[i] = hf->data + d->g.plane_off[i];
                 hf->f.width[i] = d->g.pw[i];
                 hf->f.height[i] = d->g.ph[i];
                 hf->f.stride[i] = d->g.stride[i];
             }
             hf->f.picture_coding_type = pics[p].picture_coding_type;
             hf->f.decode_index = p;
-            rc = mp2vg_download_slot(d->ctx, slot_of[p], planes, strides);
-            if (rc != MP2VG_OK) return finish(rc);
-            ready[p] = std::move(hf);
+            void* src = nullptr;
+            rc = mp2vg_slot_device_ptr(d->ctx, slot_of[p], &src);
+            if (rc == MP2VG_OK && hipMemcpyAsync(hf->data, src, d->g.slot_bytes, hipMemcpyDeviceToHost, dl) != hipSuccess)
+                rc = MP2VG_E_HIP;
+            if (rc != MP2VG_OK) {
+                pool.put(hf);
+                return finish(rc);
+            }
+            ready[p] = hf;
         }
+        if (hipStreamSynchronize(dl) != hipSuccess) return finish(MP2VG_E_HIP);
+        t_down += now_ms() - tc;
         // release slots no later picture predicts from
         for (int p = 0; p < e; p++)
             if (slot_of[p] >= 0 && last_use[p] < e) {
@@ -192,12 +250,17 @@ extern "C" int mp2vg_decoder_decode(mp2vg_decoder_t* d, const uint8_t* buf, uint
             auto it = ready.find(display[next_display]);
             {
                 std::lock_guard<std::mutex> lk(mu);
-                q.push_back(std::move(it->second));
+                q.push_back(it->second);
             }
             cv.notify_one();
             ready.erase(it);
             next_display++;
         }
     }
-    return finish(next_display == display.size() ? MP2VG_OK : MP2VG_E_STATE);
+    rc = finish(next_display == display.size() ? MP2VG_OK : MP2VG_E_STATE);
+    trace_phase("dropin: upload (sum)", now_ms() - t_up);
+    trace_phase("dropin: decode (sum)", now_ms() - t_dec);
+    trace_phase("dropin: download (sum)", now_ms() - t_down);
+    trace_phase("dropin: after parse", t0);
+    return rc;
 }

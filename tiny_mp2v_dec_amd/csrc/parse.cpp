@@ -90,6 +90,7 @@ void parse_slice(const Ctx& C, const PicWork& P, const SliceJob& job, mp2vg_mb_t
     const int cf = C.g.cf;
     const int nblocks = C.g.nblocks;
     BitReader br(C.buf + job.byte_off, C.buf + job.byte_end);
+    out.coefs.reserve(4096);
 
     // slice header (mp2v_hdr.h:345-363)
     br.skip(24);
@@ -312,7 +313,7 @@ void parse_slice(const Ctx& C, const PicWork& P, const SliceJob& job, mp2vg_mb_t
         if (intra && h.intra_vlc_format == 0)
             FAIL(MP2VG_E_UNSUPPORTED, "intra macroblock with intra_vlc_format=0 (reference mis-parses)");
         const int tab = intra ? 1 : 0;
-        const VlcLut& cl = T.coef[tab];
+        const CoefLut& cf_lut = T.coefs[tab];
         for (int b = 0; b < nblocks; b++) {
             if (!(cbp & (1u << b))) continue;
             int i = 0;
@@ -343,18 +344,14 @@ void parse_slice(const Ctx& C, const PicWork& P, const SliceJob& job, mp2vg_mb_t
                 }
             }
             for (;;) {
-                int ci = cl.decode(br);
-                if (ci < 0) FAIL(MP2VG_E_BITSTREAM, "bad DCT coefficient code");
-                if (ci == Tables::COEF_EOB) break;
                 int run, level;
-                if (ci == Tables::COEF_ESC) {
+                const int kind = cf_lut.decode(br, run, level);
+                if (kind < 0) FAIL(MP2VG_E_BITSTREAM, "bad DCT coefficient code");
+                if (kind == CoefLut::EOB) break;
+                if (kind == CoefLut::ESC) {
                     run = (int)br.read(6);
                     int v = (int)br.read(12);
                     level = (v & 0x800) ? v - 4096 : v;  // signed 12-bit (:100-104)
-                } else {
-                    run = T.coef_run[tab][ci];
-                    level = T.coef_level[tab][ci];
-                    if (br.read(1)) level = -level;
                 }
                 i += run;
                 if (i > 63) FAIL(MP2VG_E_BITSTREAM, "coefficient run past position 63");
@@ -375,10 +372,31 @@ void parse_slice(const Ctx& C, const PicWork& P, const SliceJob& job, mp2vg_mb_t
 
 }  // namespace
 
+// allocator whose resize() leaves new elements uninitialised (the coefficient array is filled
+// completely by the parallel concatenation; zeroing it first would be a serial memset)
+template <class T>
+struct NoInitAlloc : std::allocator<T> {
+    template <class U>
+    struct rebind {
+        using other = NoInitAlloc<U>;
+    };
+    NoInitAlloc() = default;
+    template <class U>
+    NoInitAlloc(const NoInitAlloc<U>&) {}
+    template <class U>
+    void construct(U* p) {
+        ::new ((void*)p) U;
+    }
+    template <class U, class... A>
+    void construct(U* p, A&&... a) {
+        ::new ((void*)p) U(std::forward<A>(a)...);
+    }
+};
+
 struct ParsedImpl {
     std::vector<mp2vg_picture_t> pics;
     std::vector<mp2vg_mb_t> mbs;
-    std::vector<uint32_t> coefs;
+    std::vector<uint32_t, NoInitAlloc<uint32_t>> coefs;
     std::vector<int32_t> display;
     std::vector<int32_t> gop;
 };
@@ -403,13 +421,20 @@ extern "C" int mp2vg_parse_es(const uint8_t* buf, uint64_t len, const mp2vg_conf
     C.mbh = cfg->height / 16;
     C.g.init(cfg->width, cfg->height, cfg->chroma_format);
 
+    double tp = now_ms();
     // ---- pass 1: start codes and headers, serially (decoder.cpp:278-329) ----
     std::vector<uint64_t> sc;
-    for (uint64_t i = 0; i + 3 < len; i++)
-        if (buf[i] == 0 && buf[i + 1] == 0 && buf[i + 2] == 1) {
-            sc.push_back(i);
-            i += 2;
+    for (uint64_t i = 0; i + 3 < len;) {  // 00 00 01: find each 01 byte with memchr
+        const void* hit = memchr(buf + i + 2, 1, len - 1 - (i + 2));
+        if (!hit) break;
+        const uint64_t k = (uint64_t)((const uint8_t*)hit - buf);  // buf[k] == 1, k >= i + 2
+        if (buf[k - 1] == 0 && buf[k - 2] == 0) {
+            sc.push_back(k - 2);
+            i = k + 1;
+        } else {
+            i = k - 1;
         }
+    }
     int seq_chroma = -1;
     int cur = -1;
     int gop = -1;
@@ -508,6 +533,7 @@ extern "C" int mp2vg_parse_es(const uint8_t* buf, uint64_t len, const mp2vg_conf
         if (P.slices.empty()) { set_error("picture without slices"); return MP2VG_E_BITSTREAM; }
         build_W(h.qme, h.alternate_scan, P.W);
     }
+    tp = trace_phase("parse: headers", tp);
     // ---- pass 2: slices (independent given picture state) in parallel ----
     const int npics = (int)C.pics.size();
     const size_t mbs_per_pic = (size_t)C.mbw * C.mbh;
@@ -563,26 +589,39 @@ extern "C" int mp2vg_parse_es(const uint8_t* buf, uint64_t len, const mp2vg_conf
                 delete res;
                 return MP2VG_E_UNSUPPORTED;
             }
-    // ---- concatenate coefficients, fix offsets ----
-    size_t total = 0;
-    for (auto& o : outs) total += o.coefs.size();
+    tp = trace_phase("parse: slices", tp);
+    // ---- concatenate coefficients, fix offsets: prefix sum, then copies in parallel ----
+    std::vector<size_t> base(jobs.size() + 1, 0);
+    for (size_t j = 0; j < jobs.size(); j++) base[j + 1] = base[j] + outs[j].coefs.size();
+    const size_t total = base[jobs.size()];
     if (total >= (1ull << 32)) {
         delete res;
         set_error("batch too large");
         return MP2VG_E_INVALID;
     }
     res->coefs.resize(total);
-    {
-        size_t base = 0;
-        for (size_t j = 0; j < jobs.size(); j++) {
-            const SliceOut& o = outs[j];
-            if (!o.coefs.empty()) memcpy(&res->coefs[base], o.coefs.data(), o.coefs.size() * 4);
-            int p = jobs[j].pic;
-            mp2vg_mb_t* row = res->mbs.data() + mbs_per_pic * p + (size_t)o.mb_row * C.mbw;
-            for (int x = 0; x < C.mbw; x++) row[x].coef_off += (uint32_t)base;
-            base += o.coefs.size();
+    std::atomic<int> next_cp(0);
+    auto copier = [&]() {
+        for (;;) {
+            const int p = next_cp.fetch_add(1);
+            if (p >= npics) return;
+            for (size_t j = pic_job_begin[p]; j < pic_job_begin[p + 1]; j++) {
+                SliceOut& o = outs[j];
+                if (!o.coefs.empty()) memcpy(&res->coefs[base[j]], o.coefs.data(), o.coefs.size() * 4);
+                mp2vg_mb_t* row = res->mbs.data() + mbs_per_pic * p + (size_t)o.mb_row * C.mbw;
+                for (int x = 0; x < C.mbw; x++) row[x].coef_off += (uint32_t)base[j];
+                std::vector<uint32_t>().swap(o.coefs);
+            }
         }
+    };
+    if (nthreads == 1) {
+        copier();
+    } else {
+        std::vector<std::thread> th;
+        for (int t = 0; t < nthreads; t++) th.emplace_back(copier);
+        for (auto& t : th) t.join();
     }
+    tp = trace_phase("parse: concatenate", tp);
     // ---- picture records ----
     res->pics.resize(npics);
     for (int p = 0; p < npics; p++) {

@@ -12,6 +12,8 @@
 #include <cstring>
 #include <string>
 #include <vector>
+#include <atomic>
+#include <thread>
 
 #include "recon_kernel.h"
 #include "syntax.h"
@@ -63,6 +65,7 @@ struct mp2vg_ctx {
 
     std::vector<hipEvent_t> ev;   // 2 per launch (start, end; on the launch's stream)
     hipEvent_t evb[2] = {nullptr, nullptr};  // whole batch, main stream
+    hipEvent_t up_ev[2] = {nullptr, nullptr};  // staging halves of upload()
     int nlaunch = 0;
 
     void* h_stage = nullptr;
@@ -82,18 +85,24 @@ static int grow(T*& p, size_t& cap, size_t n) {
     return MP2VG_OK;
 }
 
+// Host -> device copy through the pinned staging buffer, double-buffered: the memcpy of the next
+// half overlaps the DMA of the previous one.
 static int upload(mp2vg_ctx_t* ctx, void* dst, const void* src, size_t bytes) {
     const uint8_t* s = (const uint8_t*)src;
     uint8_t* d = (uint8_t*)dst;
-    while (bytes) {
-        size_t n = std::min(bytes, kStageBytes);
-        memcpy(ctx->h_stage, s, n);
-        HIPCHK(hipMemcpyAsync(d, ctx->h_stage, n, hipMemcpyHostToDevice, ctx->stream));
-        HIPCHK(hipStreamSynchronize(ctx->stream));
+    const size_t half = kStageBytes / 2;
+    for (int i = 0; bytes; i++) {
+        const size_t n = std::min(bytes, half);
+        uint8_t* st = (uint8_t*)ctx->h_stage + (i & 1) * half;
+        if (i >= 2) HIPCHK(hipEventSynchronize(ctx->up_ev[i & 1]));
+        memcpy(st, s, n);
+        HIPCHK(hipMemcpyAsync(d, st, n, hipMemcpyHostToDevice, ctx->stream));
+        HIPCHK(hipEventRecord(ctx->up_ev[i & 1], ctx->stream));
         s += n;
         d += n;
         bytes -= n;
     }
+    HIPCHK(hipStreamSynchronize(ctx->stream));
     return MP2VG_OK;
 }
 
@@ -113,6 +122,8 @@ extern "C" int mp2vg_create(const mp2vg_config_t* cfg, mp2vg_ctx_t** out) {
     c->g.init(cfg->width, cfg->height, cfg->chroma_format);
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->evb[0]) != hipSuccess || hipEventCreate(&c->evb[1]) != hipSuccess ||
+        hipEventCreateWithFlags(&c->up_ev[0], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->up_ev[1], hipEventDisableTiming) != hipSuccess ||
         hipHostMalloc(&c->h_stage, kStageBytes, hipHostMallocDefault) != hipSuccess) {
         set_error("stream / pinned staging allocation failed");
         delete c;
@@ -133,6 +144,8 @@ extern "C" int mp2vg_destroy(mp2vg_ctx_t* c) {
     if (c->stream) hipStreamSynchronize(c->stream);
     for (auto e : c->ev) hipEventDestroy(e);
     for (auto e : c->evb)
+        if (e) hipEventDestroy(e);
+    for (auto e : c->up_ev)
         if (e) hipEventDestroy(e);
 
     hipFree(c->d_pool);
@@ -178,59 +191,65 @@ static int plan_batch(mp2vg_ctx_t* c, const mp2vg_picture_t* pics, int32_t npics
     std::vector<int> level(npics, 0);
     std::vector<int> last_write(c->nslots, -1), max_read(c->nslots, -1);
     int maxlevel = -1;
-    for (int p = 0; p < npics; p++) {
+    // per-picture record validation (O(MBs + coefficient words)) runs on host threads; the first
+    // failing picture in batch order reports its error
+    std::vector<uint8_t> uses_of(2 * (size_t)npics, 0);
+    std::vector<const char*> err(npics, nullptr);
+    auto validate = [&](int p) -> const char* {
         const mp2vg_picture_t& P = pics[p];
-        if (P.mb_width != mbw || P.mb_height != mbh) {
-            set_error("picture size differs from the context geometry");
-            return MP2VG_E_INVALID;
-        }
-        if (P.dst_slot < 0 || P.dst_slot >= c->nslots || P.fwd_slot >= c->nslots || P.bwd_slot >= c->nslots) {
-            set_error("frame slot out of range (mp2vg_reserve_slots)");
-            return MP2VG_E_INVALID;
-        }
-        uint64_t nm = (uint64_t)mbw * mbh;
-        if ((uint64_t)P.mb_first + nm > nmbs) {
-            set_error("picture MB range outside the batch");
-            return MP2VG_E_INVALID;
-        }
+        if (P.mb_width != mbw || P.mb_height != mbh) return "picture size differs from the context geometry";
+        if (P.dst_slot < 0 || P.dst_slot >= c->nslots || P.fwd_slot >= c->nslots || P.bwd_slot >= c->nslots)
+            return "frame slot out of range (mp2vg_reserve_slots)";
+        const uint64_t nm = (uint64_t)mbw * mbh;
+        if ((uint64_t)P.mb_first + nm > nmbs) return "picture MB range outside the batch";
         bool uses[2] = {false, false};
         for (uint64_t k = 0; k < nm; k++) {
             const mp2vg_mb_t& m = mbs[P.mb_first + k];
-            if (m.x != k % mbw || m.y != k / mbw) {
-                set_error("MB records not in raster order");
-                return MP2VG_E_INVALID;
-            }
-            if ((uint64_t)m.coef_off + m.ncoef > ncoefs) {
-                set_error("MB coefficient range outside the batch");
-                return MP2VG_E_INVALID;
-            }
+            if (m.x != k % mbw || m.y != k / mbw) return "MB records not in raster order";
+            if ((uint64_t)m.coef_off + m.ncoef > ncoefs) return "MB coefficient range outside the batch";
             // the kernel takes a word's MB (inside its 8-MB group) from bits 28-30
             const uint32_t tag = MP2VG_COEF_MBX(m.x);
-            for (uint32_t j = 0; j < m.ncoef; j++) {
-                if ((coefs[m.coef_off + j] & 0xF0000000u) != tag) {
-                    set_error("coefficient word bits 28-31 are not the MB column mod 8");
-                    return MP2VG_E_INVALID;
-                }
-            }
+            uint32_t bad = 0;
+            const uint32_t* w = coefs + m.coef_off;
+            for (uint32_t j = 0; j < m.ncoef; j++) bad |= (w[j] & 0xF0000000u) ^ tag;
+            if (bad) return "coefficient word bits 28-31 are not the MB column mod 8";
             // the kernel streams the coefficient words of consecutive MBs of a row as one range
             if (k % mbw != 0) {
                 const mp2vg_mb_t& pm = mbs[P.mb_first + k - 1];
-                if ((uint64_t)pm.coef_off + pm.ncoef != m.coef_off) {
-                    set_error("coefficient words of a macroblock row are not contiguous");
-                    return MP2VG_E_INVALID;
-                }
+                if ((uint64_t)pm.coef_off + pm.ncoef != m.coef_off)
+                    return "coefficient words of a macroblock row are not contiguous";
             }
-            if (m.cbp >> nb) {
-                set_error("cbp names a block the chroma format does not have");
-                return MP2VG_E_INVALID;
-            }
+            if (m.cbp >> nb) return "cbp names a block the chroma format does not have";
             if (!(m.flags & MP2VG_MB_INTRA)) {
-                bool f = (m.flags & MP2VG_MB_FWD) || !(m.flags & MP2VG_MB_BWD);
-                bool b = m.flags & MP2VG_MB_BWD;
-                uses[0] |= f;
-                uses[1] |= b;
+                uses[0] |= (m.flags & MP2VG_MB_FWD) || !(m.flags & MP2VG_MB_BWD);
+                uses[1] |= (m.flags & MP2VG_MB_BWD) != 0;
             }
         }
+        uses_of[2 * (size_t)p] = uses[0];
+        uses_of[2 * (size_t)p + 1] = uses[1];
+        return nullptr;
+    };
+    {
+        const int nth = std::max(1, std::min({npics, 16, (int)std::thread::hardware_concurrency()}));
+        std::atomic<int> next(0);
+        auto worker = [&]() {
+            for (int p; (p = next.fetch_add(1)) < npics;) err[p] = validate(p);
+        };
+        if (nth == 1) {
+            worker();
+        } else {
+            std::vector<std::thread> th;
+            for (int t = 0; t < nth; t++) th.emplace_back(worker);
+            for (auto& t : th) t.join();
+        }
+    }
+    for (int p = 0; p < npics; p++) {
+        const mp2vg_picture_t& P = pics[p];
+        if (err[p]) {
+            set_error(err[p]);
+            return MP2VG_E_INVALID;
+        }
+        const bool uses[2] = {uses_of[2 * (size_t)p] != 0, uses_of[2 * (size_t)p + 1] != 0};
         if ((uses[0] && P.fwd_slot < 0) || (uses[1] && P.bwd_slot < 0)) {
             set_error("picture predicts from a missing reference slot");
             return MP2VG_E_INVALID;

@@ -26,7 +26,20 @@ struct BitReader {
     BitReader() = default;
     BitReader(const uint8_t* b, const uint8_t* e) : base(b), p(b), end(e) {}
 
+    // Keeps >= 32 valid bits after a refill.  Fast path: one unaligned 8-byte big-endian load
+    // adds as many whole bytes as fit; near the end of the buffer, bytes past `end` read as 0.
     inline void refill() {
+        if (bits > 32) return;
+        if (p + 8 <= end) {
+            uint64_t v;
+            memcpy(&v, p, 8);
+            v = __builtin_bswap64(v);
+            const int k = (63 - bits) >> 3;  // 3..7 whole bytes
+            cache |= (v >> (8 * (8 - k))) << (64 - bits - 8 * k);
+            p += k;
+            bits += 8 * k;
+            return;
+        }
         while (bits <= 56) {
             uint64_t byte = (p < end) ? *p : 0;
             cache |= byte << (56 - bits);
@@ -34,12 +47,18 @@ struct BitReader {
             bits += 8;
         }
     }
-    inline uint32_t peek(int n) {
+    inline uint32_t peek(int n) {  // n <= 32
         if (n == 0) return 0;
         refill();
         return (uint32_t)(cache >> (64 - n));
     }
     inline void skip(int n) {
+        while (n > 32) {
+            refill();
+            cache <<= 32;
+            bits -= 32;
+            n -= 32;
+        }
         refill();
         cache <<= n;
         bits -= n;
@@ -110,11 +129,35 @@ struct VlcLut {
     }
 };
 
+// DCT coefficient decoder (B.14 / B.15) with the sign bit folded in: one 10-bit lookup decodes
+// the common short codes completely; longer codes take a second 7-bit lookup.
+// Entry: bits 0-4 bits consumed (0 = invalid), 5-10 run, 11-22 signed level, 23-24 kind.
+struct CoefLut {
+    enum { NORMAL = 0, EOB = 1, ESC = 2, SUB = 3, L1 = 10, L2 = 7 };
+    std::vector<uint32_t> l1, l2;  // l2: 128-entry sub-tables
+    static uint32_t pack(int len, int run, int level, int kind) {
+        return (uint32_t)len | ((uint32_t)run << 5) | (((uint32_t)level & 0xfff) << 11) | ((uint32_t)kind << 23);
+    }
+    // code: '0'/'1' string; sign appended for NORMAL codes
+    void add(const char* bits, int run, int level, int kind);
+    // returns kind; run / level / consumes the code (and the sign bit)
+    inline int decode(BitReader& br, int& run, int& level) const {
+        uint32_t e = l1[br.peek(L1)];
+        if (((e >> 23) & 3) == SUB) {
+            br.skip(L1);
+            e = l2[((e >> 5) & 0x3ffff) * 128 + br.peek(L2)];
+        }
+        if (!(e & 31)) return -1;
+        br.skip((int)(e & 31));
+        run = (int)((e >> 5) & 63);
+        level = (int)((int32_t)(e << 9) >> 20);  // sign-extend bits 11-22
+        return (int)((e >> 23) & 3);
+    }
+};
+
 struct Tables {
-    VlcLut mba, mbtype[4], cbp, motion, dc_luma, dc_chroma, coef[2];
-    // coefficient LUT payload: index into run/level arrays; special indices
-    enum { COEF_EOB = 1000, COEF_ESC = 1001 };
-    std::vector<int> coef_run[2], coef_level[2];
+    VlcLut mba, mbtype[4], cbp, motion, dc_luma, dc_chroma;
+    CoefLut coefs[2];
     static const Tables& get();
 };
 
@@ -226,5 +269,10 @@ inline bool mc_reads_inside(const Geom& g, int mbx, int mby, int mvx, int mvy, b
 }
 
 void set_error(const std::string& msg);
+
+// Host phase timing for diagnosis: with MP2VG_TRACE set, trace_phase(name, t0) prints the
+// milliseconds since t0 to stderr and returns the current time.
+double now_ms();
+double trace_phase(const char* name, double t0);
 
 }  // namespace mp2vg

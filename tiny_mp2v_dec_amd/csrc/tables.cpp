@@ -1,3 +1,6 @@
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 // tables.cpp — decode LUTs built once from the Annex B code lists in vlc_tables.h, scan tables,
 // error plumbing shared by the whole library.
 #include <mutex>
@@ -22,6 +25,38 @@ static void add_list(VlcLut& l, const vlc_code (&codes)[N]) {
     for (int i = 0; i < N; i++) l.add(codes[i].bits, i);
 }
 
+void CoefLut::add(const char* bits, int run, int level, int kind) {
+    const int len = (int)strlen(bits);
+    for (int sign = 0; sign < (kind == NORMAL ? 2 : 1); sign++) {
+        uint32_t code = 0;
+        for (int i = 0; i < len; i++) code = (code << 1) | (bits[i] == '1');
+        int n = len;
+        int lv = level;
+        if (kind == NORMAL) {
+            code = (code << 1) | (uint32_t)sign;
+            n++;
+            lv = sign ? -level : level;
+        }
+        if (n <= L1) {
+            const uint32_t lo = code << (L1 - n), hi = (code + 1) << (L1 - n);
+            for (uint32_t v = lo; v < hi; v++) l1[v] = pack(n, run, lv, kind);
+        } else {
+            const uint32_t pre = code >> (n - L1);
+            uint32_t& e = l1[pre];
+            if (((e >> 23) & 3) != SUB) {
+                const uint32_t idx = (uint32_t)(l2.size() / 128);
+                l2.resize(l2.size() + 128, 0);
+                e = pack(0, 0, 0, SUB) | (idx << 5);
+            }
+            const uint32_t idx = (e >> 5) & 0x3ffff;
+            const int m = n - L1;  // <= L2
+            const uint32_t rest = code & ((1u << m) - 1);
+            const uint32_t lo = rest << (L2 - m), hi = (rest + 1) << (L2 - m);
+            for (uint32_t v = lo; v < hi; v++) l2[idx * 128 + v] = pack(m, run, lv, kind);
+        }
+    }
+}
+
 static Tables* build_tables() {
     Tables* t = new Tables();
     t->mba.init(11);
@@ -42,17 +77,13 @@ static Tables* build_tables() {
     t->dc_chroma.init(10);
     add_list(t->dc_chroma, kDcSizeChroma);
     for (int tab = 0; tab < 2; tab++) {
-        VlcLut& l = t->coef[tab];
-        l.init(16);
         const vlc_code* codes = tab == 0 ? kCoeffZero : kCoeffOne;
-        int n = tab == 0 ? countof(kCoeffZero) : countof(kCoeffOne);
-        for (int i = 0; i < n; i++) {
-            l.add(codes[i].bits, i);
-            t->coef_run[tab].push_back(codes[i].a);
-            t->coef_level[tab].push_back(codes[i].b);
-        }
-        l.add(tab == 0 ? kCoeffZeroEob : kCoeffOneEob, Tables::COEF_EOB);
-        l.add(kCoeffEscape, Tables::COEF_ESC);
+        const int n = tab == 0 ? countof(kCoeffZero) : countof(kCoeffOne);
+        CoefLut& f = t->coefs[tab];
+        f.l1.assign(1u << CoefLut::L1, 0);
+        for (int i = 0; i < n; i++) f.add(codes[i].bits, codes[i].a, codes[i].b, CoefLut::NORMAL);
+        f.add(tab == 0 ? kCoeffZeroEob : kCoeffOneEob, 0, 0, CoefLut::EOB);
+        f.add(kCoeffEscape, 0, 0, CoefLut::ESC);
     }
     return t;
 }
@@ -60,6 +91,16 @@ static Tables* build_tables() {
 const Tables& Tables::get() {
     static Tables* t = build_tables();
     return *t;
+}
+
+double now_ms() {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+double trace_phase(const char* name, double t0) {
+    static const bool on = getenv("MP2VG_TRACE") != nullptr;
+    const double t = now_ms();
+    if (on) fprintf(stderr, "[mp2vg] %-24s %9.3f ms\n", name, t - t0);
+    return t;
 }
 
 static thread_local std::string g_last_error;
