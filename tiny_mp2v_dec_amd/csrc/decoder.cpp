@@ -91,7 +91,8 @@ extern "C" int mp2vg_decoder_create(const mp2vg_config_t* cfg, mp2vg_render_fn f
     if (!cfg || !fn || !out) return MP2VG_E_INVALID;
     *out = nullptr;
     mp2vg_config_t c = *cfg;
-    c.pictures_pool_size = std::max(cfg->pictures_pool_size, kChunk + 4);
+    // chunk k decodes into its own slots while chunk k-1 is still being downloaded
+    c.pictures_pool_size = std::max(cfg->pictures_pool_size, 2 * kChunk + 4);
     mp2vg_ctx_t* ctx = nullptr;
     int rc = mp2vg_create(&c, &ctx);
     if (rc != MP2VG_OK) return rc;
@@ -172,6 +173,7 @@ extern "C" int mp2vg_decoder_decode(mp2vg_decoder_t* d, const uint8_t* buf, uint
     const uint64_t mbs_per_pic = (uint64_t)(d->cfg.width / 16) * (d->cfg.height / 16);
 
     auto finish = [&](int status) {
+        hipStreamSynchronize(dl);  // no copy may still target a pool frame
         {
             std::lock_guard<std::mutex> lk(mu);
             done = true;
@@ -181,10 +183,45 @@ extern "C" int mp2vg_decoder_decode(mp2vg_decoder_t* d, const uint8_t* buf, uint
         return status;
     };
 
+    // Chunk pipeline: the D2H copies of chunk k-1 (stream dl) run while chunk k is uploaded and
+    // decoded.  A chunk's frames reach the renderer, and its slots return to the free list, only
+    // after its copies have completed.
+    std::map<int, HostFrame*> inflight;  // decode index -> frame whose copy is in flight
+    int pend_e = -1;                     // end of the chunk whose copies are in flight
+    int decoded_e = 0;                   // pictures [0, decoded_e) are decoded
+    auto complete_pending = [&]() -> int {
+        if (pend_e < 0) return MP2VG_OK;
+        tc = now_ms();
+        if (hipStreamSynchronize(dl) != hipSuccess) return MP2VG_E_HIP;
+        t_down += now_ms() - tc;
+        for (auto& kv : inflight) ready[kv.first] = kv.second;
+        inflight.clear();
+        // release slots no later picture predicts from
+        for (int p = 0; p < pend_e; p++)
+            if (slot_of[p] >= 0 && last_use[p] < decoded_e) {
+                free_slots.push_back(slot_of[p]);
+                slot_of[p] = -1;
+            }
+        pend_e = -1;
+        // hand frames to the render thread in display order
+        while (next_display < display.size() && ready.count(display[next_display])) {
+            auto it = ready.find(display[next_display]);
+            {
+                std::lock_guard<std::mutex> lk(mu);
+                q.push_back(it->second);
+            }
+            cv.notify_one();
+            ready.erase(it);
+            next_display++;
+        }
+        return MP2VG_OK;
+    };
+
     for (int s = 0; s < npics; s += kChunk) {
         int e = std::min(npics, s + kChunk);
-        // slots for this chunk
+        // slots for this chunk (the previous chunk's copies finish first when the pool runs dry)
         for (int p = s; p < e; p++) {
+            if (free_slots.empty() && (rc = complete_pending()) != MP2VG_OK) return finish(rc);
             if (free_slots.empty()) return finish(MP2VG_E_STATE);
             slot_of[p] = free_slots.back();
             free_slots.pop_back();
@@ -213,9 +250,10 @@ extern "C" int mp2vg_decoder_decode(mp2vg_decoder_t* d, const uint8_t* buf, uint
         if (rc == MP2VG_OK) rc = mp2vg_batch_decode(d->ctx);
         if (rc == MP2VG_OK) rc = mp2vg_synchronize(d->ctx);
         t_dec += now_ms() - tc;
-        tc = now_ms();
         if (rc != MP2VG_OK) return finish(rc);
-        // download into frame_c-layout host frames: one DMA per slot, one wait per chunk
+        decoded_e = e;
+        if ((rc = complete_pending()) != MP2VG_OK) return finish(rc);
+        // copies of this chunk into frame_c-layout host frames: one DMA per slot
         for (int p = s; p < e; p++) {
             HostFrame* hf = pool.get();
             if (!hf) return finish(MP2VG_E_NOMEM);
@@ -235,28 +273,11 @@ extern "C" int mp2vg_decoder_decode(mp2vg_decoder_t* d, const uint8_t* buf, uint
                 pool.put(hf);
                 return finish(rc);
             }
-            ready[p] = hf;
+            inflight[p] = hf;
         }
-        if (hipStreamSynchronize(dl) != hipSuccess) return finish(MP2VG_E_HIP);
-        t_down += now_ms() - tc;
-        // release slots no later picture predicts from
-        for (int p = 0; p < e; p++)
-            if (slot_of[p] >= 0 && last_use[p] < e) {
-                free_slots.push_back(slot_of[p]);
-                slot_of[p] = -1;
-            }
-        // hand frames to the render thread in display order
-        while (next_display < display.size() && ready.count(display[next_display])) {
-            auto it = ready.find(display[next_display]);
-            {
-                std::lock_guard<std::mutex> lk(mu);
-                q.push_back(it->second);
-            }
-            cv.notify_one();
-            ready.erase(it);
-            next_display++;
-        }
+        pend_e = e;
     }
+    if ((rc = complete_pending()) != MP2VG_OK) return finish(rc);
     rc = finish(next_display == display.size() ? MP2VG_OK : MP2VG_E_STATE);
     trace_phase("dropin: upload (sum)", now_ms() - t_up);
     trace_phase("dropin: decode (sum)", now_ms() - t_dec);
