@@ -503,6 +503,7 @@ struct Lds {
     short blk[WAVES][MAXS][BLKS];
     short res[WAVES][G * ResLayout<CF>::SIZE];
     uint8_t map[WAVES][MAXS];                    // slot -> k*16 + b
+    uint32_t dq[WAVES][64];                      // (k*16 + b) -> dequant parameters (DqEntry)
     uint8_t W[4][64];
     uint8_t scan[64];
 };
@@ -518,25 +519,40 @@ struct SliceCtx {
     uint32_t mb_begin, mb_end;
 };
 
+// Per-group dequant parameters of block b of MB k, built once per group by lane k*16 + b:
+// bits 0-7 coded-block slot, 8-15 quantiser_scale, 16-17 quantiser matrix (W row), 18 intra,
+// 19 coded (cbp bit set and b < NB).
+template <int CF>
+__device__ __forceinline__ uint32_t dq_entry(const Group& S, int lane) {
+    constexpr int NB = Fmt<CF>::NB;
+    const int k = lane >> 4, bb = lane & 15;
+    const uint32_t cbpk = pick16(S.cbp01, S.cbp23, k);
+    const bool coded = bb < NB && ((cbpk >> bb) & 1);
+    const uint32_t slot = pick8(S.sb8, k) + (uint32_t)__builtin_popcount(cbpk & ((1u << bb) - 1));
+    const uint32_t intra = pick8(S.fl8, k) & MP2VG_MB_INTRA;
+    const uint32_t wsel = (bb < 6 ? 0u : 2u) + (intra ? 0u : 1u);
+    return (slot & 0xff) | (pick8(S.qs8, k) << 8) | (wsel << 16) | (intra << 18) | ((uint32_t)coded << 19);
+}
+
 // dequant of one coefficient word (parse_block, mb_decoder.cpp:74-155) into its coded-block
-// slot: lane = word, MB k from the word's MB-column bits
+// slot: lane = word; its MB k (from the word's MB-column bits) and block select the group's
+// dequant entry
 template <int CF>
 __device__ __forceinline__ void dequant_word(Lds<CF>& L, int wave, const Group& S, uint32_t w) {
-    constexpr int NB = Fmt<CF>::NB;
     const int k = (int)(((w >> 28) - S.x0) & 7u);  // MB column bits (include/mp2vg.h), checked on upload
-    const uint32_t cbpk = pick16(S.cbp01, S.cbp23, k);
     const int bb = (w >> 22) & 15;
-    if (bb >= NB || !(cbpk & (1u << bb))) return;  // host validation rejects these
-    const int slot = (int)pick8(S.sb8, k) + __builtin_popcount(cbpk & ((1u << bb) - 1));
-    const bool intra = pick8(S.fl8, k) & MP2VG_MB_INTRA;
-    const int qs = (int)pick8(S.qs8, k);
+    const uint32_t e = L.dq[wave][(k & 3) * 16 + bb];
+    if (k > 3 || !(e & (1u << 19))) return;  // host validation rejects these
+    const int slot = (int)(e & 0xff);
+    const bool intra = (e >> 18) & 1;
+    const int qs = (int)((e >> 8) & 0xff);
     const int i = (w >> 16) & 63;
     const int level = (short)(w & 0xffff);
     if (w & MP2VG_COEF_DC) {  // QFS[0] = dc << (3 - prec), outside the parity sum (:160)
         L.blk[wave][slot][0] = (short)level;
         return;
     }
-    const int Wi = L.W[(bb < 6 ? 0 : 2) + (intra ? 0 : 1)][i];
+    const int Wi = L.W[(e >> 16) & 3][i];
     const int sign = level < 0 ? -1 : 0;
     const int mag = level < 0 ? -level : level;
     short v;
@@ -668,12 +684,12 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, Lds
 
         stamp<ABL>(st, 1);
         // ---- C. slot map + dequant (parse_block, mb_decoder.cpp:74-155) ----
-        if (lane < Lds<CF>::MAXS) {
-            const int k = lane / NB, bb = lane % NB;
-            const uint32_t cbpk = pick16(S.cbp01, S.cbp23, k);
-            if (cbpk & (1u << bb))
-                L.map[wave][(int)pick8(S.sb8, k) + __builtin_popcount(cbpk & ((1u << bb) - 1))] = (uint8_t)(k * 16 + bb);
+        {
+            const uint32_t e = dq_entry<CF>(S, lane);
+            L.dq[wave][lane] = e;
+            if (e & (1u << 19)) L.map[wave][e & 0xff] = (uint8_t)lane;
         }
+        wave_sync();
         if (!(ABL & 4)) {
             // words 0..64*NCW-1 from the registers loaded one group ahead; more (rare) loaded here
 #pragma unroll
