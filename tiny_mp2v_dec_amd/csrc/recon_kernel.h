@@ -36,6 +36,7 @@ struct Launch {
     uint32_t begin, end;
     int mcm;
     int level;  // dependency level: launches of one level may run concurrently
+    int set;    // independent picture set (its own stream)
 };
 
 // per-launch geometry, passed by value

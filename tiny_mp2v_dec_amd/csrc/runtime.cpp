@@ -43,11 +43,16 @@ static constexpr size_t kSinkOff = 2048;
 static constexpr size_t kCoefPad = 256;        // the kernel prefetches up to 256 coefficient words per MB group
 static constexpr size_t kStageBytes = 32u << 20;
 static constexpr size_t kMbPad = 16;  // >= the kernel's MB group size
+// independent picture sets per batch, one stream each (c2: 1 set 2.575 ms, 2 sets 2.502-2.535 ms,
+// 3 sets 2.566, 4 sets 2.590; MP2VG_STREAMS overrides for measurements)
+static const int kStreams = getenv("MP2VG_STREAMS") ? std::max(1, atoi(getenv("MP2VG_STREAMS"))) : 2;
 
 struct mp2vg_ctx {
     mp2vg_config_t cfg{};
     Geom g{};
-    hipStream_t stream = nullptr;
+    hipStream_t stream = nullptr;  // set 0's stream; every API call synchronises on it
+    std::vector<hipStream_t> sstreams;  // sets 1.. (created on first use)
+    std::vector<hipEvent_t> sev;        // end of each set's launches
     uint8_t* d_pool = nullptr;
     int32_t nslots = 0;
 
@@ -156,6 +161,8 @@ extern "C" int mp2vg_destroy(mp2vg_ctx_t* c) {
     hipFree(c->d_dslots);
     hipFree(c->d_digest);
     if (c->h_stage) hipHostFree(c->h_stage);
+    for (auto e : c->sev) hipEventDestroy(e);
+    for (auto st : c->sstreams) hipStreamDestroy(st);
     if (c->stream) hipStreamDestroy(c->stream);
     delete c;
     return MP2VG_OK;
@@ -276,16 +283,50 @@ static int plan_batch(mp2vg_ctx_t* c, const mp2vg_picture_t* pics, int32_t npics
     // runs the mixed kernel, which picks the mode per workgroup from the picture type: one launch
     // tail per level instead of one per type.  Pictures stay in decode order, so every XCD's
     // contiguous share of the slices holds the same mix of P and B work.
-    std::vector<std::vector<int>> bylevel(maxlevel + 1);
-    for (int p = 0; p < npics; p++) bylevel[level[p]].push_back(p);
+    //
+    // Independent picture sets run on separate streams: pictures that touch a common slot (as
+    // destination or used reference) are one component; components (closed GOPs) are dealt to
+    // kStreams sets, each with its own chain of level launches.  The streams run freely, so one
+    // set's VALU-heavy I level overlaps another's memory-heavy B level and fills its launch tails.
+    const int nsets = std::max(1, std::min(kStreams, npics));
+    std::vector<int> parent(npics);
+    for (int p = 0; p < npics; p++) parent[p] = p;
+    auto find = [&](int x) {
+        while (parent[x] != x) x = parent[x] = parent[parent[x]];
+        return x;
+    };
+    {
+        std::vector<int> owner(c->nslots, -1);
+        for (int p = 0; p < npics; p++) {
+            const mp2vg_picture_t& P = pics[p];
+            const int sl[3] = {P.dst_slot, uses_of[2 * (size_t)p] ? P.fwd_slot : -1,
+                               uses_of[2 * (size_t)p + 1] ? P.bwd_slot : -1};
+            for (int s : sl) {
+                if (s < 0) continue;
+                if (owner[s] < 0) owner[s] = p;
+                else parent[find(p)] = find(owner[s]);
+            }
+        }
+    }
+    std::vector<int> set_of(npics, 0), root_set(npics, -1);
+    std::vector<size_t> load(nsets, 0);
+    for (int p = 0; p < npics; p++) {  // components in decode order of their first picture
+        const int r = find(p);
+        if (root_set[r] < 0) root_set[r] = (int)(std::min_element(load.begin(), load.end()) - load.begin());
+        set_of[p] = root_set[r];
+        load[set_of[p]]++;
+    }
     slices.clear();
     launches.clear();
-    for (size_t q = 0; q < bylevel.size(); q++) {
-        if (bylevel[q].empty()) continue;
+    for (int set = 0; set < nsets; set++)
+    for (int q = 0; q <= maxlevel; q++) {
+        std::vector<int> lp;
+        for (int p = 0; p < npics; p++)
+            if (level[p] == q && set_of[p] == set) lp.push_back(p);
+        if (lp.empty()) continue;
         Launch l;
         l.begin = (uint32_t)slices.size();
         int types = 0;
-        const std::vector<int>& lp = bylevel[q];
         for (int p : lp) {
             const int pct = pics[p].picture_coding_type;
             types |= 1 << (pct == 1 ? 0 : (pct == 2 ? 1 : 2));
@@ -312,7 +353,8 @@ static int plan_batch(mp2vg_ctx_t* c, const mp2vg_picture_t* pics, int32_t npics
         }
         l.end = (uint32_t)slices.size();
         l.mcm = types == 1 ? 0 : (types == 2 ? 1 : (types == 4 ? 2 : 3));
-        l.level = (int)q;
+        l.level = q;
+        l.set = set;
         launches.push_back(l);
     }
     return MP2VG_OK;
@@ -372,16 +414,33 @@ extern "C" int mp2vg_batch_decode(mp2vg_ctx_t* c) {
         a.stride[i] = c->g.stride[i];
         a.ph[i] = c->g.ph[i];
     }
-    // Launches run back to back on one stream (dependency levels in order; within a level the I/P
-    // and B launches are independent).  Overlapping a level's launches on a second stream was
-    // measured: no gain -- the fixed cost of tails and boundaries is ~0.15 ms per batch.
+    // Each picture set's level launches run back to back on its own stream; the set streams
+    // start after everything queued before this batch (evb[0]) and set 0's stream waits for all
+    // of them at the end, so API calls that synchronise on c->stream see the whole batch.
+    int nsets = 1;
+    for (const Launch& L : c->launches) nsets = std::max(nsets, L.set + 1);
+    while ((int)c->sstreams.size() < nsets - 1) {
+        hipStream_t st;
+        hipEvent_t e;
+        HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+        HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        c->sstreams.push_back(st);
+        c->sev.push_back(e);
+    }
+    auto stream_of = [&](int set) { return set == 0 ? c->stream : c->sstreams[set - 1]; };
     HIPCHK(hipEventRecord(c->evb[0], c->stream));
+    for (int set = 1; set < nsets; set++) HIPCHK(hipStreamWaitEvent(stream_of(set), c->evb[0], 0));
     for (int i = 0; i < nl; i++) {
+        const hipStream_t st = stream_of(c->launches[i].set);
         a.slice_base = c->launches[i].begin;
         a.nslices = c->launches[i].end - c->launches[i].begin;
-        HIPCHK(hipEventRecord(c->ev[2 * i], c->stream));
-        if (a.nslices) HIPCHK(launch_recon(c->g.cf, c->launches[i].mcm, a, c->stream));
-        HIPCHK(hipEventRecord(c->ev[2 * i + 1], c->stream));
+        HIPCHK(hipEventRecord(c->ev[2 * i], st));
+        if (a.nslices) HIPCHK(launch_recon(c->g.cf, c->launches[i].mcm, a, st));
+        HIPCHK(hipEventRecord(c->ev[2 * i + 1], st));
+    }
+    for (int set = 1; set < nsets; set++) {
+        HIPCHK(hipEventRecord(c->sev[set - 1], stream_of(set)));
+        HIPCHK(hipStreamWaitEvent(c->stream, c->sev[set - 1], 0));
     }
     HIPCHK(hipEventRecord(c->evb[1], c->stream));
     c->nlaunch = nl;
