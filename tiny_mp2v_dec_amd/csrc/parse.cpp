@@ -19,6 +19,9 @@
 #include <cstdlib>
 #include <string>
 #include <thread>
+#include <memory>
+#include <condition_variable>
+#include <mutex>
 #include <vector>
 
 #include "syntax.h"
@@ -395,7 +398,7 @@ struct NoInitAlloc : std::allocator<T> {
 
 struct ParsedImpl {
     std::vector<mp2vg_picture_t> pics;
-    std::vector<mp2vg_mb_t> mbs;
+    std::vector<mp2vg_mb_t, NoInitAlloc<mp2vg_mb_t>> mbs;  // every record is written by its slice
     std::vector<uint32_t, NoInitAlloc<uint32_t>> coefs;
     std::vector<int32_t> display;
     std::vector<int32_t> gop;
@@ -407,12 +410,81 @@ struct mp2vg_parsed : mp2vg::ParsedImpl {};
 
 using namespace mp2vg;
 
-extern "C" int mp2vg_parse_es(const uint8_t* buf, uint64_t len, const mp2vg_config_t* cfg,
-                              mp2vg_parsed_t** out) {
+// ---- parse session: pass 1 on the caller's thread, pass 2 on worker threads ---------------
+// Workers claim pictures in decode order; a picture's slices are parsed by one worker, which
+// then publishes the picture (status + its MB records).  mp2vg_parse_es waits for all of them;
+// the drop-in decoder consumes pictures as they complete (decoder.cpp), overlapping the parse
+// with the device work.
+struct ParseSession {
+    Ctx C;
+    mp2vg_parsed* res = nullptr;  // pictures, MB records (coef_off relative to the slice), display
+    std::vector<SliceJob> jobs;
+    std::vector<SliceOut> outs;
+    std::vector<std::vector<uint8_t>> row_done;
+    std::vector<size_t> pic_job_begin;
+    std::vector<int> status;  // per picture: 1 pending, else an MP2VG_* status
+    std::vector<std::string> err;
+    std::mutex mu;
+    std::condition_variable cv;
+    std::atomic<int> next_pic{0};
+    std::vector<std::thread> workers;
+    size_t mbs_per_pic = 0;
+
+    ~ParseSession() {
+        join();
+        delete res;
+    }
+    void join() {
+        for (auto& t : workers) t.join();
+        workers.clear();
+    }
+    void work() {
+        const int npics = (int)C.pics.size();
+        for (;;) {
+            const int p = next_pic.fetch_add(1);
+            if (p >= npics) return;
+            int st = MP2VG_OK;
+            std::string msg;
+            for (size_t j = pic_job_begin[p]; j < pic_job_begin[p + 1]; j++) {
+                parse_slice(C, C.pics[p], jobs[j], res->mbs.data() + mbs_per_pic * p, row_done[p], outs[j]);
+                if (outs[j].status != MP2VG_OK && st == MP2VG_OK) {
+                    char m[256];
+                    snprintf(m, sizeof m, "picture %d slice @%llu: %s", p, (unsigned long long)jobs[j].byte_off,
+                             outs[j].err.c_str());
+                    st = outs[j].status;
+                    msg = m;
+                }
+            }
+            if (st == MP2VG_OK)
+                for (int r = 0; r < C.mbh; r++)
+                    if (!row_done[p][r]) {
+                        st = MP2VG_E_UNSUPPORTED;
+                        msg = "picture with a macroblock row not covered by any slice";
+                        break;
+                    }
+            {
+                std::lock_guard<std::mutex> lk(mu);
+                status[p] = st;
+                err[p] = msg;
+            }
+            cv.notify_all();
+        }
+    }
+    int wait(int p) {
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [&] { return status[p] != 1; });
+        if (status[p] != MP2VG_OK) set_error(err[p]);
+        return status[p];
+    }
+};
+
+int parse_session_start(const uint8_t* buf, uint64_t len, const mp2vg_config_t* cfg, int threads,
+                        ParseSession** out) {
     if (!buf || !cfg || !out) return MP2VG_E_INVALID;
     *out = nullptr;
     if (mp2vg_frame_geometry(cfg, nullptr, nullptr, nullptr, nullptr) != MP2VG_OK) return MP2VG_E_INVALID;
-    Ctx C;
+    std::unique_ptr<ParseSession> S(new ParseSession());
+    Ctx& C = S->C;
     C.buf = buf;
     C.len = len;
     C.width = cfg->width;
@@ -534,94 +606,27 @@ extern "C" int mp2vg_parse_es(const uint8_t* buf, uint64_t len, const mp2vg_conf
         build_W(h.qme, h.alternate_scan, P.W);
     }
     tp = trace_phase("parse: headers", tp);
-    // ---- pass 2: slices (independent given picture state) in parallel ----
     const int npics = (int)C.pics.size();
     const size_t mbs_per_pic = (size_t)C.mbw * C.mbh;
+    S->mbs_per_pic = mbs_per_pic;
     auto* res = new mp2vg_parsed();
+    S->res = res;
     res->mbs.resize(mbs_per_pic * npics);
-    std::vector<SliceJob> jobs;
     for (auto& P : C.pics)
-        for (auto& j : P.slices) jobs.push_back(j);
-    std::vector<SliceOut> outs(jobs.size());
-    std::vector<std::vector<uint8_t>> row_done(npics, std::vector<uint8_t>(C.mbh, 0));
-    // rows of one picture are claimed by one thread at a time: partition jobs by picture
-    std::atomic<int> next_pic(0);
-    std::vector<size_t> pic_job_begin(npics + 1, 0);
+        for (auto& j : P.slices) S->jobs.push_back(j);
+    S->outs.resize(S->jobs.size());
+    S->row_done.assign(npics, std::vector<uint8_t>(C.mbh, 0));
+    S->pic_job_begin.assign(npics + 1, 0);
     {
         size_t j = 0;
         for (int p = 0; p < npics; p++) {
-            pic_job_begin[p] = j;
+            S->pic_job_begin[p] = j;
             j += C.pics[p].slices.size();
         }
-        pic_job_begin[npics] = j;
+        S->pic_job_begin[npics] = j;
     }
-    int nthreads = cfg->num_threads > 0 ? cfg->num_threads : (int)std::thread::hardware_concurrency();
-    nthreads = std::max(1, std::min(nthreads, std::max(1, npics)));
-    auto worker = [&]() {
-        for (;;) {
-            int p = next_pic.fetch_add(1);
-            if (p >= npics) return;
-            for (size_t j = pic_job_begin[p]; j < pic_job_begin[p + 1]; j++)
-                parse_slice(C, C.pics[p], jobs[j], res->mbs.data() + mbs_per_pic * p, row_done[p], outs[j]);
-        }
-    };
-    if (nthreads == 1) {
-        worker();
-    } else {
-        std::vector<std::thread> th;
-        for (int t = 0; t < nthreads; t++) th.emplace_back(worker);
-        for (auto& t : th) t.join();
-    }
-    for (size_t j = 0; j < jobs.size(); j++)
-        if (outs[j].status != MP2VG_OK) {
-            char msg[256];
-            snprintf(msg, sizeof msg, "picture %d slice @%llu: %s", jobs[j].pic,
-                     (unsigned long long)jobs[j].byte_off, outs[j].err.c_str());
-            set_error(msg);
-            int st = outs[j].status;
-            delete res;
-            return st;
-        }
-    for (int p = 0; p < npics; p++)
-        for (int r = 0; r < C.mbh; r++)
-            if (!row_done[p][r]) {
-                set_error("picture with a macroblock row not covered by any slice");
-                delete res;
-                return MP2VG_E_UNSUPPORTED;
-            }
-    tp = trace_phase("parse: slices", tp);
-    // ---- concatenate coefficients, fix offsets: prefix sum, then copies in parallel ----
-    std::vector<size_t> base(jobs.size() + 1, 0);
-    for (size_t j = 0; j < jobs.size(); j++) base[j + 1] = base[j] + outs[j].coefs.size();
-    const size_t total = base[jobs.size()];
-    if (total >= (1ull << 32)) {
-        delete res;
-        set_error("batch too large");
-        return MP2VG_E_INVALID;
-    }
-    res->coefs.resize(total);
-    std::atomic<int> next_cp(0);
-    auto copier = [&]() {
-        for (;;) {
-            const int p = next_cp.fetch_add(1);
-            if (p >= npics) return;
-            for (size_t j = pic_job_begin[p]; j < pic_job_begin[p + 1]; j++) {
-                SliceOut& o = outs[j];
-                if (!o.coefs.empty()) memcpy(&res->coefs[base[j]], o.coefs.data(), o.coefs.size() * 4);
-                mp2vg_mb_t* row = res->mbs.data() + mbs_per_pic * p + (size_t)o.mb_row * C.mbw;
-                for (int x = 0; x < C.mbw; x++) row[x].coef_off += (uint32_t)base[j];
-                std::vector<uint32_t>().swap(o.coefs);
-            }
-        }
-    };
-    if (nthreads == 1) {
-        copier();
-    } else {
-        std::vector<std::thread> th;
-        for (int t = 0; t < nthreads; t++) th.emplace_back(copier);
-        for (auto& t : th) t.join();
-    }
-    tp = trace_phase("parse: concatenate", tp);
+    S->status.assign(npics, 1);
+    S->err.assign(npics, std::string());
     // ---- picture records ----
     res->pics.resize(npics);
     for (int p = 0; p < npics; p++) {
@@ -653,6 +658,88 @@ extern "C" int mp2vg_parse_es(const uint8_t* buf, uint64_t len, const mp2vg_conf
         }
         if (held >= 0) res->display.push_back(held);
     }
+    int nthreads = threads > 0 ? threads : (int)std::thread::hardware_concurrency();
+    nthreads = std::max(1, std::min(nthreads, std::max(1, npics)));
+    ParseSession* sp = S.get();
+    for (int t = 0; t < nthreads; t++) sp->workers.emplace_back([sp]() { sp->work(); });
+    *out = S.release();
+    return MP2VG_OK;
+}
+
+int parse_session_npics(const ParseSession* s) { return (int)s->C.pics.size(); }
+const mp2vg_picture_t* parse_session_pictures(const ParseSession* s) { return s->res->pics.data(); }
+const int32_t* parse_session_display(const ParseSession* s) { return s->res->display.data(); }
+int parse_session_wait(ParseSession* s, int p) { return s->wait(p); }
+void parse_session_free(ParseSession* s) { delete s; }
+
+// Picture p (after parse_session_wait): its MB records with coef_off relative to `coefs`, which
+// receives the picture's coefficient words appended at `coef_base` (its current size).
+void parse_session_append(ParseSession* s, int p, mp2vg_mb_t* mbs_out, std::vector<uint32_t>& coefs) {
+    const size_t n = s->mbs_per_pic;
+    memcpy(mbs_out, s->res->mbs.data() + n * p, n * sizeof(mp2vg_mb_t));
+    for (size_t j = s->pic_job_begin[p]; j < s->pic_job_begin[p + 1]; j++) {
+        const SliceOut& o = s->outs[j];
+        const uint32_t base = (uint32_t)coefs.size();
+        coefs.insert(coefs.end(), o.coefs.begin(), o.coefs.end());
+        mp2vg_mb_t* row = mbs_out + (size_t)o.mb_row * s->C.mbw;
+        for (int x = 0; x < s->C.mbw; x++) row[x].coef_off += base;
+    }
+}
+
+extern "C" int mp2vg_parse_es(const uint8_t* buf, uint64_t len, const mp2vg_config_t* cfg,
+                              mp2vg_parsed_t** out) {
+    if (!out) return MP2VG_E_INVALID;
+    *out = nullptr;
+    ParseSession* sp = nullptr;
+    int rc = parse_session_start(buf, len, cfg, cfg ? cfg->num_threads : 0, &sp);
+    if (rc != MP2VG_OK) return rc;
+    std::unique_ptr<ParseSession> S(sp);
+    double tp = now_ms();
+    S->join();
+    const int npics = (int)S->C.pics.size();
+    for (int p = 0; p < npics; p++)
+        if ((rc = S->wait(p)) != MP2VG_OK) return rc;
+    tp = trace_phase("parse: slices", tp);
+    // ---- concatenate coefficients, fix offsets: prefix sum, then copies in parallel ----
+    std::vector<SliceJob>& jobs = S->jobs;
+    std::vector<SliceOut>& outs = S->outs;
+    const std::vector<size_t>& pic_job_begin = S->pic_job_begin;
+    const size_t mbs_per_pic = S->mbs_per_pic;
+    mp2vg_parsed* res = S->res;
+    const Ctx& C = S->C;
+    std::vector<size_t> base(jobs.size() + 1, 0);
+    for (size_t j = 0; j < jobs.size(); j++) base[j + 1] = base[j] + outs[j].coefs.size();
+    const size_t total = base[jobs.size()];
+    if (total >= (1ull << 32)) {
+        set_error("batch too large");
+        return MP2VG_E_INVALID;
+    }
+    res->coefs.resize(total);
+    std::atomic<int> next_cp(0);
+    auto copier = [&]() {
+        for (;;) {
+            const int p = next_cp.fetch_add(1);
+            if (p >= npics) return;
+            for (size_t j = pic_job_begin[p]; j < pic_job_begin[p + 1]; j++) {
+                SliceOut& o = outs[j];
+                if (!o.coefs.empty()) memcpy(&res->coefs[base[j]], o.coefs.data(), o.coefs.size() * 4);
+                mp2vg_mb_t* row = res->mbs.data() + mbs_per_pic * p + (size_t)o.mb_row * C.mbw;
+                for (int x = 0; x < C.mbw; x++) row[x].coef_off += (uint32_t)base[j];
+                std::vector<uint32_t>().swap(o.coefs);
+            }
+        }
+    };
+    int nthreads = cfg->num_threads > 0 ? cfg->num_threads : (int)std::thread::hardware_concurrency();
+    nthreads = std::max(1, std::min(nthreads, std::max(1, npics)));
+    if (nthreads == 1) {
+        copier();
+    } else {
+        std::vector<std::thread> th;
+        for (int t = 0; t < nthreads; t++) th.emplace_back(copier);
+        for (auto& t : th) t.join();
+    }
+    tp = trace_phase("parse: concatenate", tp);
+    S->res = nullptr;
     *out = res;
     return MP2VG_OK;
 }

@@ -276,3 +276,16 @@ double now_ms();
 double trace_phase(const char* name, double t0);
 
 }  // namespace mp2vg
+
+// Streaming parse (parse.cpp): pass 1 (start codes, headers, picture records, display order) on
+// the calling thread, pass 2 (slices -> MB records + coefficient words) on `threads` workers that
+// publish pictures in about decode order.  mp2vg_parse_es and the drop-in decoder both use it.
+struct ParseSession;
+int parse_session_start(const uint8_t* buf, uint64_t len, const mp2vg_config_t* cfg, int threads,
+                        ParseSession** out);
+int parse_session_npics(const ParseSession* s);
+const mp2vg_picture_t* parse_session_pictures(const ParseSession* s);  // dst_slot = decode index
+const int32_t* parse_session_display(const ParseSession* s);           // npics entries
+int parse_session_wait(ParseSession* s, int p);  // status of picture p once its slices are parsed
+void parse_session_append(ParseSession* s, int p, mp2vg_mb_t* mbs_out, std::vector<uint32_t>& coefs);
+void parse_session_free(ParseSession* s);
