@@ -536,15 +536,16 @@ __device__ __forceinline__ uint32_t dq_entry(const Group& S, int lane) {
 
 // dequant of one coefficient word (parse_block, mb_decoder.cpp:74-155) into its coded-block
 // slot: lane = word; its MB k (from the word's MB-column bits) and block select the group's
-// dequant entry
-template <int CF>
+// dequant entry.  INTRA_ONLY (I pictures: every MB intra, no '1s' first coefficients) drops the
+// non-intra arithmetic.
+template <int CF, bool INTRA_ONLY = false>
 __device__ __forceinline__ void dequant_word(Lds<CF>& L, int wave, const Group& S, uint32_t w) {
     const int k = (int)(((w >> 28) - S.x0) & 7u);  // MB column bits (include/mp2vg.h), checked on upload
     const int bb = (w >> 22) & 15;
     const uint32_t e = L.dq[wave][(k & 3) * 16 + bb];
     if (k > 3 || !(e & (1u << 19))) return;  // host validation rejects these
     const int slot = (int)(e & 0xff);
-    const bool intra = (e >> 18) & 1;
+    const bool intra = INTRA_ONLY || ((e >> 18) & 1);
     const int qs = (int)((e >> 8) & 0xff);
     const int i = (w >> 16) & 63;
     const int level = (short)(w & 0xffff);
@@ -557,7 +558,7 @@ __device__ __forceinline__ void dequant_word(Lds<CF>& L, int wave, const Group& 
     const int mag = level < 0 ? -level : level;
     short v;
     int pos;
-    if (w & MP2VG_COEF_FIRST1S) {  // (3*W*qs)>>5 at qfs[0], unclamped (:79-88)
+    if (!INTRA_ONLY && (w & MP2VG_COEF_FIRST1S)) {  // (3*W*qs)>>5 at qfs[0], unclamped (:79-88)
         const short t = (short)((3 * Wi * qs) >> 5);
         v = (short)((t ^ sign) - sign);
         pos = 0;
@@ -694,7 +695,7 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, Lds
             // words 0..64*NCW-1 from the registers loaded one group ahead; more (rare) loaded here
 #pragma unroll
             for (int j = 0; j < NCW; j++)
-                if (64 * j + lane < S.ncoef) dequant_word<CF>(L, wave, S, cw[j]);
+                if (64 * j + lane < S.ncoef) dequant_word<CF, MCM == 0>(L, wave, S, cw[j]);
             // words past the prefetch: XW loads per lane in flight per round trip, not one (a 4:4:4
             // intra group carries ~1,400 words)
             constexpr int XW = MCM == 0 ? 8 : 2;
@@ -707,7 +708,7 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, Lds
                 }
 #pragma unroll
                 for (int j = 0; j < XW; j++)
-                    if (base + 64 * j + lane < S.ncoef) dequant_word<CF>(L, wave, S, xw[j]);
+                    if (base + 64 * j + lane < S.ncoef) dequant_word<CF, MCM == 0>(L, wave, S, xw[j]);
             }
         }
         // first 64*NCW coefficient words of g+1 (the words of g are consumed)
