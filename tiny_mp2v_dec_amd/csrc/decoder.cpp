@@ -28,12 +28,24 @@
 
 using namespace mp2vg;
 
+namespace mp2vg {
+int batch_upload_pinned(mp2vg_ctx_t* c, const mp2vg_picture_t* pics, int32_t npics, const mp2vg_mb_t* mbs,
+                        uint64_t nmbs, const uint32_t* coefs, uint64_t ncoefs);
+hipStream_t ctx_stream(mp2vg_ctx_t* c);
+int ctx_next_bank(const mp2vg_ctx_t* c);
+int ctx_wait_upload(mp2vg_ctx_t* c, int bank);
+void ctx_set_launch_timing(mp2vg_ctx_t* c, bool on);
+}  // namespace mp2vg
+
 namespace {
-constexpr int kChunk = 16;  // pictures per device batch
+// pictures per device batch (MP2VG_CHUNK overrides it for measurements)
+const int kChunk = getenv("MP2VG_CHUNK") ? std::max(1, atoi(getenv("MP2VG_CHUNK"))) : 16;
 
 // Host frames live in pinned memory, in the device slot layout (= the reference frame_c layout),
 // so a decoded slot comes back with one contiguous DMA copy.  They are recycled after the render
 // callback returns (a frame is valid only during the callback, reference threads.cpp:75-80).
+// The pool belongs to the decoder and is filled when it is created, as the reference allocates
+// its picture pool up front (decoder.cpp:381-406).
 struct HostFrame {
     uint8_t* data = nullptr;
     mp2vg_frame_t f;
@@ -48,6 +60,14 @@ class FramePool {
             delete f;
         }
     }
+    bool reserve(int n) {
+        while ((int)all_.size() < n) {
+            HostFrame* f = alloc();
+            if (!f) return false;
+            put(f);
+        }
+        return true;
+    }
     HostFrame* get() {
         {
             std::lock_guard<std::mutex> lk(mu_);
@@ -57,6 +77,15 @@ class FramePool {
                 return f;
             }
         }
+        return alloc();
+    }
+    void put(HostFrame* f) {
+        std::lock_guard<std::mutex> lk(mu_);
+        free_.push_back(f);
+    }
+
+  private:
+    HostFrame* alloc() {
         auto* f = new HostFrame();
         if (hipHostMalloc((void**)&f->data, bytes_, hipHostMallocDefault) != hipSuccess) {
             delete f;
@@ -66,15 +95,31 @@ class FramePool {
         all_.push_back(f);
         return f;
     }
-    void put(HostFrame* f) {
-        std::lock_guard<std::mutex> lk(mu_);
-        free_.push_back(f);
-    }
-
-  private:
     size_t bytes_;
     std::mutex mu_;
     std::vector<HostFrame*> all_, free_;
+};
+
+// Growable pinned host buffer: a chunk's records are gathered here and DMA'd without staging.
+struct PinnedBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    ~PinnedBuf() {
+        if (p) hipHostFree(p);
+    }
+    bool reserve(size_t bytes) {
+        if (bytes <= cap) return true;
+        const size_t c = std::max(bytes, cap + cap / 2);
+        if (p) hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+        if (hipHostMalloc(&p, c, hipHostMallocDefault) != hipSuccess) {
+            p = nullptr;
+            return false;
+        }
+        cap = c;
+        return true;
+    }
 };
 }  // namespace
 
@@ -85,7 +130,23 @@ struct mp2vg_decoder {
     mp2vg_ctx_t* ctx = nullptr;
     Geom g{};
     int nslots = 0;
+    std::unique_ptr<FramePool> pool;
+    PinnedBuf mbuf[2], cbuf[2];        // chunk MB records / coefficient words, one set per record bank
+    hipStream_t dl = nullptr;          // frame downloads
+    hipEvent_t decoded = nullptr;      // end of the last chunk's decode (on the context stream)
 };
+
+extern "C" int mp2vg_decoder_destroy(mp2vg_decoder_t* d) {
+    if (!d) return MP2VG_E_INVALID;
+    if (d->dl) hipStreamSynchronize(d->dl);
+    if (d->ctx) mp2vg_synchronize(d->ctx);
+    d->pool.reset();
+    if (d->decoded) hipEventDestroy(d->decoded);
+    if (d->dl) hipStreamDestroy(d->dl);
+    if (d->ctx) mp2vg_destroy(d->ctx);
+    delete d;
+    return MP2VG_OK;
+}
 
 extern "C" int mp2vg_decoder_create(const mp2vg_config_t* cfg, mp2vg_render_fn fn, void* user,
                                     mp2vg_decoder_t** out) {
@@ -104,14 +165,27 @@ extern "C" int mp2vg_decoder_create(const mp2vg_config_t* cfg, mp2vg_render_fn f
     d->ctx = ctx;
     d->g.init(c.width, c.height, c.chroma_format);
     d->nslots = c.pictures_pool_size;
+    d->pool.reset(new FramePool(d->g.slot_bytes));
+    ctx_set_launch_timing(ctx, false);  // no per-launch events on the drop-in's chunk path
+    if (hipStreamCreateWithFlags(&d->dl, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&d->decoded, hipEventDisableTiming) != hipSuccess) {
+        set_error("download stream / event creation failed");
+        mp2vg_decoder_destroy(d);
+        return MP2VG_E_HIP;
+    }
+    // chunk record buffers sized up front: every MB record of a chunk, and 32 coefficient words
+    // per MB (the bench stream needs 12.5; a chunk that needs more grows its set once)
+    const size_t chunk_mbs = (size_t)kChunk * (c.width / 16) * (c.height / 16);
+    bool ok = true;
+    for (int i = 0; i < 2; i++)
+        ok = ok && d->mbuf[i].reserve(chunk_mbs * sizeof(mp2vg_mb_t)) && d->cbuf[i].reserve(chunk_mbs * 32 * 4);
+    // frames in flight: one chunk being copied, one being rendered, anchors held for display
+    if (!ok || !d->pool->reserve(2 * kChunk + 4)) {
+        set_error("pinned host frame allocation failed");
+        mp2vg_decoder_destroy(d);
+        return MP2VG_E_NOMEM;
+    }
     *out = d;
-    return MP2VG_OK;
-}
-
-extern "C" int mp2vg_decoder_destroy(mp2vg_decoder_t* d) {
-    if (!d) return MP2VG_E_INVALID;
-    mp2vg_destroy(d->ctx);
-    delete d;
     return MP2VG_OK;
 }
 
@@ -120,7 +194,7 @@ extern "C" int mp2vg_decoder_decode(mp2vg_decoder_t* d, const uint8_t* buf, uint
     // the parse runs on worker threads while the chunks below go through the device: a chunk
     // waits only for its own pictures (two threads are left for this loop and the renderer)
     double t0 = now_ms(), tc;
-    double t_up = 0, t_dec = 0, t_down = 0, t_wait = 0;
+    double t_up = 0, t_dec = 0, t_down = 0, t_wait = 0, t_gather = 0;
     ParseSession* ps = nullptr;
     const int threads = d->cfg.num_threads > 0 ? d->cfg.num_threads : (int)std::thread::hardware_concurrency();
     // (16-thread box: 2 or 4 threads kept back 1,975 frames/s, 1 -> 1,864, 6 -> 1,661)
@@ -144,10 +218,8 @@ extern "C" int mp2vg_decoder_decode(mp2vg_decoder_t* d, const uint8_t* buf, uint
     std::condition_variable cv;
     std::deque<HostFrame*> q;
     bool done = false;
-    FramePool pool(d->g.slot_bytes);
-    hipStream_t dl = nullptr;
-    if (hipStreamCreateWithFlags(&dl, hipStreamNonBlocking) != hipSuccess) return MP2VG_E_HIP;
-    std::unique_ptr<void, void (*)(void*)> dl_guard(dl, [](void* s) { hipStreamDestroy((hipStream_t)s); });
+    FramePool& pool = *d->pool;
+    hipStream_t dl = d->dl;
     std::thread render([&]() {
         for (;;) {
             HostFrame* f;
@@ -169,12 +241,13 @@ extern "C" int mp2vg_decoder_decode(mp2vg_decoder_t* d, const uint8_t* buf, uint
     std::map<int, HostFrame*> ready;  // decode index -> downloaded frame
     size_t next_display = 0;
     std::vector<mp2vg_picture_t> cp;
-    std::vector<mp2vg_mb_t> cm;
-    std::vector<uint32_t> cc;
+    std::vector<size_t> ncoef_of(kChunk);
+    std::vector<uint32_t> base_of(kChunk);
     const uint64_t mbs_per_pic = (uint64_t)(d->cfg.width / 16) * (d->cfg.height / 16);
 
     auto finish = [&](int status) {
         hipStreamSynchronize(dl);  // no copy may still target a pool frame
+        mp2vg_synchronize(d->ctx);
         {
             std::lock_guard<std::mutex> lk(mu);
             done = true;
@@ -184,12 +257,16 @@ extern "C" int mp2vg_decoder_decode(mp2vg_decoder_t* d, const uint8_t* buf, uint
         return status;
     };
 
-    // Chunk pipeline: the D2H copies of chunk k-1 (stream dl) run while chunk k is uploaded and
-    // decoded.  A chunk's frames reach the renderer, and its slots return to the free list, only
-    // after its copies have completed.
+    // Chunk pipeline, nothing waits for the device except through an event:
+    //   host:   gather chunk k's records (pinned) | upload (copy stream; waits only for the decode
+    //           of chunk k-2, which read the same record bank) | queue decode k | complete k-1
+    //   device: decode k-1 ... decode k (context stream) while the D2H copies of k-1 run (dl)
+    // A chunk's frames reach the renderer, and its slots return to the free list, only after its
+    // copies have completed; a released slot is rewritten only by a later chunk, whose decode is
+    // ordered after every earlier decode on the context stream.
     std::map<int, HostFrame*> inflight;  // decode index -> frame whose copy is in flight
     int pend_e = -1;                     // end of the chunk whose copies are in flight
-    int decoded_e = 0;                   // pictures [0, decoded_e) are decoded
+    int decoded_e = 0;                   // the decodes of pictures [0, decoded_e) are queued
     auto complete_pending = [&]() -> int {
         if (pend_e < 0) return MP2VG_OK;
         tc = now_ms();
@@ -227,33 +304,50 @@ extern "C" int mp2vg_decoder_decode(mp2vg_decoder_t* d, const uint8_t* buf, uint
             slot_of[p] = free_slots.back();
             free_slots.pop_back();
         }
-        // chunk records with physical slots; MB and coefficient offsets local to the chunk
+        // chunk records with physical slots; MB and coefficient offsets local to the chunk,
+        // gathered straight into pinned memory
         cp.assign(pics + s, pics + e);
-        cm.resize((size_t)(e - s) * mbs_per_pic);
-        cc.clear();
         tc = now_ms();
+        size_t nc = 0;
         for (int p = s; p < e; p++) {
             if ((rc = parse_session_wait(ps, p)) != MP2VG_OK) return finish(rc);
-            parse_session_append(ps, p, cm.data() + (size_t)(p - s) * mbs_per_pic, cc);
+            ncoef_of[p - s] = parse_session_ncoefs(ps, p);
+            nc += ncoef_of[p - s];
         }
         t_wait += now_ms() - tc;
+        const size_t nm = (size_t)(e - s) * mbs_per_pic;
+        tc = now_ms();
+        // this chunk's buffer set fed the upload two chunks back: its copies must have landed
+        const int hb = ctx_next_bank(d->ctx);
+        if ((rc = ctx_wait_upload(d->ctx, hb)) != MP2VG_OK) return finish(rc);
+        if (nc >= (1ull << 32) || !d->mbuf[hb].reserve(nm * sizeof(mp2vg_mb_t)) ||
+            !d->cbuf[hb].reserve(std::max<size_t>(nc, 1) * 4))
+            return finish(MP2VG_E_NOMEM);
+        auto* cm = (mp2vg_mb_t*)d->mbuf[hb].p;
+        auto* cc = (uint32_t*)d->cbuf[hb].p;
+        for (int i = 0, base = 0; i < e - s; base += (int)ncoef_of[i], i++) base_of[i] = (uint32_t)base;
+        parallel_for(e - s, 8, [&](int i) {
+            parse_session_append(ps, s + i, cm + (size_t)i * mbs_per_pic, cc + base_of[i], base_of[i]);
+        });
         for (auto& P : cp) {
             P.dst_slot = slot_of[P.dst_slot];
             if (P.fwd_slot >= 0) P.fwd_slot = slot_of[P.fwd_slot];
             if (P.bwd_slot >= 0) P.bwd_slot = slot_of[P.bwd_slot];
             P.mb_first = (uint32_t)((P.mb_first / mbs_per_pic - (uint64_t)s) * mbs_per_pic);
         }
+        t_gather += now_ms() - tc;
         tc = now_ms();
-        rc = mp2vg_batch_upload(d->ctx, cp.data(), (int32_t)cp.size(), cm.data(), cm.size(), cc.data(), cc.size());
+        rc = batch_upload_pinned(d->ctx, cp.data(), (int32_t)cp.size(), cm, nm, cc, nc);
         t_up += now_ms() - tc;
         tc = now_ms();
         if (rc == MP2VG_OK) rc = mp2vg_batch_decode(d->ctx);
-        if (rc == MP2VG_OK) rc = mp2vg_synchronize(d->ctx);
+        if (rc == MP2VG_OK && hipEventRecord(d->decoded, ctx_stream(d->ctx)) != hipSuccess) rc = MP2VG_E_HIP;
         t_dec += now_ms() - tc;
         if (rc != MP2VG_OK) return finish(rc);
         decoded_e = e;
         if ((rc = complete_pending()) != MP2VG_OK) return finish(rc);
-        // copies of this chunk into frame_c-layout host frames: one DMA per slot
+        // copies of this chunk into frame_c-layout host frames, one DMA per slot, after its decode
+        if (hipStreamWaitEvent(dl, d->decoded, 0) != hipSuccess) return finish(MP2VG_E_HIP);
         for (int p = s; p < e; p++) {
             HostFrame* hf = pool.get();
             if (!hf) return finish(MP2VG_E_NOMEM);
@@ -280,9 +374,10 @@ extern "C" int mp2vg_decoder_decode(mp2vg_decoder_t* d, const uint8_t* buf, uint
     if ((rc = complete_pending()) != MP2VG_OK) return finish(rc);
     rc = finish(next_display == display.size() ? MP2VG_OK : MP2VG_E_STATE);
     trace_phase("dropin: parse wait (sum)", now_ms() - t_wait);
+    trace_phase("dropin: gather (sum)", now_ms() - t_gather);
     trace_phase("dropin: upload (sum)", now_ms() - t_up);
-    trace_phase("dropin: decode (sum)", now_ms() - t_dec);
-    trace_phase("dropin: download (sum)", now_ms() - t_down);
+    trace_phase("dropin: decode issue (sum)", now_ms() - t_dec);
+    trace_phase("dropin: download wait (sum)", now_ms() - t_down);
     trace_phase("dropin: after parse", t0);
     return rc;
 }

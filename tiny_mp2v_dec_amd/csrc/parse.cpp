@@ -61,8 +61,31 @@ struct PicWork {
     std::vector<SliceJob> slices;
 };
 
+// allocator whose resize() leaves new elements uninitialised (the coefficient array is filled
+// completely by the parallel concatenation; zeroing it first would be a serial memset)
+template <class T>
+struct NoInitAlloc : std::allocator<T> {
+    template <class U>
+    struct rebind {
+        using other = NoInitAlloc<U>;
+    };
+    NoInitAlloc() = default;
+    template <class U>
+    NoInitAlloc(const NoInitAlloc<U>&) {}
+    template <class U>
+    void construct(U* p) {
+        ::new ((void*)p) U;
+    }
+    template <class U, class... A>
+    void construct(U* p, A&&... a) {
+        ::new ((void*)p) U(std::forward<A>(a)...);
+    }
+};
+
+using CoefVec = std::vector<uint32_t, NoInitAlloc<uint32_t>>;
+
 struct SliceOut {
-    std::vector<uint32_t> coefs;
+    CoefVec coefs;  // grown without zeroing; written through a raw pointer
     int mb_row = -1;
     int status = MP2VG_OK;
     std::string err;
@@ -317,9 +340,15 @@ void parse_slice(const Ctx& C, const PicWork& P, const SliceJob& job, mp2vg_mb_t
             FAIL(MP2VG_E_UNSUPPORTED, "intra macroblock with intra_vlc_format=0 (reference mis-parses)");
         const int tab = intra ? 1 : 0;
         const CoefLut& cf_lut = T.coefs[tab];
+        // room for the MB's worst case (64 words per coded block), written through a raw pointer
+        const size_t n0 = out.coefs.size();
+        out.coefs.resize(n0 + 64 * (size_t)__builtin_popcount(cbp));
+        uint32_t* w = out.coefs.data() + n0;
+        const uint32_t mbx_tag = MP2VG_COEF_MBX(x);
         for (int b = 0; b < nblocks; b++) {
             if (!(cbp & (1u << b))) continue;
             int i = 0;
+            const uint32_t btag = ((uint32_t)b << 22) | mbx_tag;  // MP2VG_COEF_PACK's block field
             if (intra) {
                 // parse_dct_dc_coeff (mb_decoder.cpp:46-72)
                 int pidx = b < 4 ? 0 : ((b & 1) ? 2 : 1);
@@ -334,34 +363,33 @@ void parse_slice(const Ctx& C, const PicWork& P, const SliceJob& job, mp2vg_mb_t
                 }
                 dc_pred[pidx] = (uint16_t)(dc_pred[pidx] + diff);
                 int16_t dcv = (int16_t)(dc_pred[pidx] << (3 - h.intra_dc_precision));
-                out.coefs.push_back(MP2VG_COEF_PACK(dcv, 0, b, MP2VG_COEF_DC | MP2VG_COEF_MBX(x)));
+                *w++ = MP2VG_COEF_PACK(dcv, 0, b, MP2VG_COEF_DC | MP2VG_COEF_MBX(x));
                 i = 1;
             } else {
                 // non-intra first coefficient '1s' (mb_decoder.cpp:79-88)
                 uint32_t c = br.peek(2);
                 if (c & 2) {
                     int lvl = (c & 1) ? -1 : 1;
-                    out.coefs.push_back(MP2VG_COEF_PACK(lvl, 0, b, MP2VG_COEF_FIRST1S | MP2VG_COEF_MBX(x)));
+                    *w++ = MP2VG_COEF_PACK(lvl, 0, b, MP2VG_COEF_FIRST1S | MP2VG_COEF_MBX(x));
                     br.skip(2);
                     i = 1;
                 }
             }
+            // parse_block's VLC loop (mb_decoder.cpp:89-149): one refill per code
             for (;;) {
                 int run, level;
                 const int kind = cf_lut.decode(br, run, level);
-                if (kind < 0) FAIL(MP2VG_E_BITSTREAM, "bad DCT coefficient code");
-                if (kind == CoefLut::EOB) break;
-                if (kind == CoefLut::ESC) {
-                    run = (int)br.read(6);
-                    int v = (int)br.read(12);
-                    level = (v & 0x800) ? v - 4096 : v;  // signed 12-bit (:100-104)
+                if (kind != CoefLut::NORMAL) {  // escapes come back as NORMAL (:100-104)
+                    if (kind < 0) FAIL(MP2VG_E_BITSTREAM, "bad DCT coefficient code");
+                    break;  // EOB
                 }
                 i += run;
-                if (i > 63) FAIL(MP2VG_E_BITSTREAM, "coefficient run past position 63");
-                out.coefs.push_back(MP2VG_COEF_PACK(level, i, b, MP2VG_COEF_MBX(x)));
+                if (__builtin_expect(i > 63, 0)) FAIL(MP2VG_E_BITSTREAM, "coefficient run past position 63");
+                *w++ = ((uint32_t)level & 0xffffu) | ((uint32_t)i << 16) | btag;
                 i++;
             }
         }
+        out.coefs.resize((size_t)(w - out.coefs.data()));
         size_t nc = out.coefs.size() - m.coef_off;
         m.ncoef = (uint16_t)nc;
         if (br.overrun()) FAIL(MP2VG_E_BITSTREAM, "slice overruns the buffer");
@@ -374,27 +402,6 @@ void parse_slice(const Ctx& C, const PicWork& P, const SliceJob& job, mp2vg_mb_t
 #undef FAIL
 
 }  // namespace
-
-// allocator whose resize() leaves new elements uninitialised (the coefficient array is filled
-// completely by the parallel concatenation; zeroing it first would be a serial memset)
-template <class T>
-struct NoInitAlloc : std::allocator<T> {
-    template <class U>
-    struct rebind {
-        using other = NoInitAlloc<U>;
-    };
-    NoInitAlloc() = default;
-    template <class U>
-    NoInitAlloc(const NoInitAlloc<U>&) {}
-    template <class U>
-    void construct(U* p) {
-        ::new ((void*)p) U;
-    }
-    template <class U, class... A>
-    void construct(U* p, A&&... a) {
-        ::new ((void*)p) U(std::forward<A>(a)...);
-    }
-};
 
 struct ParsedImpl {
     std::vector<mp2vg_picture_t> pics;
@@ -495,18 +502,27 @@ int parse_session_start(const uint8_t* buf, uint64_t len, const mp2vg_config_t* 
 
     double tp = now_ms();
     // ---- pass 1: start codes and headers, serially (decoder.cpp:278-329) ----
+    // start codes 00 00 01 (their 01 byte at k, 2 <= k <= len - 2), found with memchr on 8
+    // segments in parallel; each segment owns the 01 bytes inside it
     std::vector<uint64_t> sc;
-    for (uint64_t i = 0; i + 3 < len;) {  // 00 00 01: find each 01 byte with memchr
-        const void* hit = memchr(buf + i + 2, 1, len - 1 - (i + 2));
-        if (!hit) break;
-        const uint64_t k = (uint64_t)((const uint8_t*)hit - buf);  // buf[k] == 1, k >= i + 2
-        if (buf[k - 1] == 0 && buf[k - 2] == 0) {
-            sc.push_back(k - 2);
-            i = k + 1;
-        } else {
-            i = k - 1;
-        }
+    {
+        const int nseg = len > (1u << 20) ? 8 : 1;
+        std::vector<std::vector<uint64_t>> seg(nseg);
+        const uint64_t kend = len >= 2 ? len - 1 : 0;  // exclusive bound on k
+        parallel_for(nseg, nseg, [&](int j) {
+            uint64_t k = std::max<uint64_t>(2, kend * j / nseg);
+            const uint64_t hi = kend * (j + 1) / nseg;
+            while (k < hi) {
+                const void* hit = memchr(buf + k, 1, hi - k);
+                if (!hit) break;
+                k = (uint64_t)((const uint8_t*)hit - buf);
+                if (buf[k - 1] == 0 && buf[k - 2] == 0) seg[j].push_back(k - 2);
+                k++;
+            }
+        });
+        for (auto& v : seg) sc.insert(sc.end(), v.begin(), v.end());
     }
+    tp = trace_phase("parse: start codes", tp);
     int seq_chroma = -1;
     int cur = -1;
     int gop = -1;
@@ -672,17 +688,27 @@ const int32_t* parse_session_display(const ParseSession* s) { return s->res->dis
 int parse_session_wait(ParseSession* s, int p) { return s->wait(p); }
 void parse_session_free(ParseSession* s) { delete s; }
 
-// Picture p (after parse_session_wait): its MB records with coef_off relative to `coefs`, which
-// receives the picture's coefficient words appended at `coef_base` (its current size).
-void parse_session_append(ParseSession* s, int p, mp2vg_mb_t* mbs_out, std::vector<uint32_t>& coefs) {
+// Coefficient words of picture p (after parse_session_wait).
+size_t parse_session_ncoefs(const ParseSession* s, int p) {
+    size_t n = 0;
+    for (size_t j = s->pic_job_begin[p]; j < s->pic_job_begin[p + 1]; j++) n += s->outs[j].coefs.size();
+    return n;
+}
+
+// Picture p (after parse_session_wait): its MB records into mbs_out and its coefficient words
+// into coefs_out, with coef_off relative to coefs_out - base (the picture's words start at word
+// `base` of the caller's batch).  The picture's parse buffers are released.
+void parse_session_append(ParseSession* s, int p, mp2vg_mb_t* mbs_out, uint32_t* coefs_out, uint32_t base) {
     const size_t n = s->mbs_per_pic;
     memcpy(mbs_out, s->res->mbs.data() + n * p, n * sizeof(mp2vg_mb_t));
     for (size_t j = s->pic_job_begin[p]; j < s->pic_job_begin[p + 1]; j++) {
-        const SliceOut& o = s->outs[j];
-        const uint32_t base = (uint32_t)coefs.size();
-        coefs.insert(coefs.end(), o.coefs.begin(), o.coefs.end());
+        SliceOut& o = s->outs[j];
+        if (!o.coefs.empty()) memcpy(coefs_out, o.coefs.data(), o.coefs.size() * 4);
+        coefs_out += o.coefs.size();
         mp2vg_mb_t* row = mbs_out + (size_t)o.mb_row * s->C.mbw;
         for (int x = 0; x < s->C.mbw; x++) row[x].coef_off += base;
+        base += (uint32_t)o.coefs.size();
+        CoefVec().swap(o.coefs);
     }
 }
 
@@ -725,7 +751,7 @@ extern "C" int mp2vg_parse_es(const uint8_t* buf, uint64_t len, const mp2vg_conf
                 if (!o.coefs.empty()) memcpy(&res->coefs[base[j]], o.coefs.data(), o.coefs.size() * 4);
                 mp2vg_mb_t* row = res->mbs.data() + mbs_per_pic * p + (size_t)o.mb_row * C.mbw;
                 for (int x = 0; x < C.mbw; x++) row[x].coef_off += (uint32_t)base[j];
-                std::vector<uint32_t>().swap(o.coefs);
+                CoefVec().swap(o.coefs);
             }
         }
     };

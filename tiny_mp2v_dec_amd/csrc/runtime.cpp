@@ -47,15 +47,10 @@ static constexpr size_t kMbPad = 16;  // >= the kernel's MB group size
 // 3 sets 2.566, 4 sets 2.590; MP2VG_STREAMS overrides for measurements)
 static const int kStreams = getenv("MP2VG_STREAMS") ? std::max(1, atoi(getenv("MP2VG_STREAMS"))) : 2;
 
-struct mp2vg_ctx {
-    mp2vg_config_t cfg{};
-    Geom g{};
-    hipStream_t stream = nullptr;  // set 0's stream; every API call synchronises on it
-    std::vector<hipStream_t> sstreams;  // sets 1.. (created on first use)
-    std::vector<hipEvent_t> sev;        // end of each set's launches
-    uint8_t* d_pool = nullptr;
-    int32_t nslots = 0;
-
+// One resident record batch.  The context keeps two, so the upload of batch k+1 (on the copy
+// stream) overlaps the decode of batch k; an upload waits only for the decode that last read
+// the bank it overwrites (batch k-1).
+struct Bank {
     mp2vg_picture_t* d_pics = nullptr;
     size_t cap_pics = 0;
     mp2vg_mb_t* d_mbs = nullptr;
@@ -65,13 +60,31 @@ struct mp2vg_ctx {
     SliceDesc* d_slices = nullptr;
     size_t cap_slices = 0;
     std::vector<Launch> launches;  // slice ranges per (dependency level, picture type)
+    int32_t npics = 0;
+    hipEvent_t uploaded = nullptr;  // on ustream, after the bank's copies
+    hipEvent_t consumed = nullptr;  // on stream, after the last decode that read the bank
+    bool decoded = false;           // `consumed` has been recorded
+};
+
+struct mp2vg_ctx {
+    mp2vg_config_t cfg{};
+    Geom g{};
+    hipStream_t stream = nullptr;  // set 0's stream; every API call synchronises on it
+    hipStream_t ustream = nullptr;  // record uploads
+    std::vector<hipStream_t> sstreams;  // sets 1.. (created on first use)
+    std::vector<hipEvent_t> sev;        // end of each set's launches
+    uint8_t* d_pool = nullptr;
+    int32_t nslots = 0;
+
+    Bank bank[2];
+    int cur = -1;  // bank of the last upload
     bool batch_ready = false;
-    int32_t batch_pics = 0;
 
     std::vector<hipEvent_t> ev;   // 2 per launch (start, end; on the launch's stream)
     hipEvent_t evb[2] = {nullptr, nullptr};  // whole batch, main stream
     hipEvent_t up_ev[2] = {nullptr, nullptr};  // staging halves of upload()
     int nlaunch = 0;
+    bool launch_timing = true;  // per-launch events (mp2vg_last_launch_times)
 
     void* h_stage = nullptr;
     int32_t* d_dslots = nullptr;
@@ -90,9 +103,15 @@ static int grow(T*& p, size_t& cap, size_t n) {
     return MP2VG_OK;
 }
 
-// Host -> device copy through the pinned staging buffer, double-buffered: the memcpy of the next
-// half overlaps the DMA of the previous one.
-static int upload(mp2vg_ctx_t* ctx, void* dst, const void* src, size_t bytes) {
+// Host -> device copy on the copy stream.  Pageable sources go through the pinned staging
+// buffer, double-buffered (the memcpy of the next half overlaps the DMA of the previous one);
+// pinned sources (the drop-in decoder's chunk buffers) are copied directly.  The caller
+// synchronises the copy stream before its host buffers may change.
+static int upload(mp2vg_ctx_t* ctx, void* dst, const void* src, size_t bytes, bool pinned) {
+    if (pinned) {
+        if (bytes) HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->ustream));
+        return MP2VG_OK;
+    }
     const uint8_t* s = (const uint8_t*)src;
     uint8_t* d = (uint8_t*)dst;
     const size_t half = kStageBytes / 2;
@@ -101,13 +120,13 @@ static int upload(mp2vg_ctx_t* ctx, void* dst, const void* src, size_t bytes) {
         uint8_t* st = (uint8_t*)ctx->h_stage + (i & 1) * half;
         if (i >= 2) HIPCHK(hipEventSynchronize(ctx->up_ev[i & 1]));
         memcpy(st, s, n);
-        HIPCHK(hipMemcpyAsync(d, st, n, hipMemcpyHostToDevice, ctx->stream));
-        HIPCHK(hipEventRecord(ctx->up_ev[i & 1], ctx->stream));
+        HIPCHK(hipMemcpyAsync(d, st, n, hipMemcpyHostToDevice, ctx->ustream));
+        HIPCHK(hipEventRecord(ctx->up_ev[i & 1], ctx->ustream));
         s += n;
         d += n;
         bytes -= n;
     }
-    HIPCHK(hipStreamSynchronize(ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->ustream));
     return MP2VG_OK;
 }
 
@@ -125,13 +144,18 @@ extern "C" int mp2vg_create(const mp2vg_config_t* cfg, mp2vg_ctx_t** out) {
     mp2vg_ctx_t* c = new mp2vg_ctx_t();
     c->cfg = *cfg;
     c->g.init(cfg->width, cfg->height, cfg->chroma_format);
-    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+    bool ok = true;
+    for (Bank& b : c->bank)
+        ok = ok && hipEventCreateWithFlags(&b.uploaded, hipEventDisableTiming) == hipSuccess &&
+             hipEventCreateWithFlags(&b.consumed, hipEventDisableTiming) == hipSuccess;
+    if (!ok || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->ustream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->evb[0]) != hipSuccess || hipEventCreate(&c->evb[1]) != hipSuccess ||
         hipEventCreateWithFlags(&c->up_ev[0], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->up_ev[1], hipEventDisableTiming) != hipSuccess ||
         hipHostMalloc(&c->h_stage, kStageBytes, hipHostMallocDefault) != hipSuccess) {
         set_error("stream / pinned staging allocation failed");
-        delete c;
+        mp2vg_destroy(c);
         return MP2VG_E_HIP;
     }
     int rc = mp2vg_reserve_slots(c, std::max(1, cfg->pictures_pool_size));
@@ -147,6 +171,7 @@ extern "C" int mp2vg_destroy(mp2vg_ctx_t* c) {
     if (!c) return MP2VG_E_INVALID;
     hipSetDevice(c->cfg.device);
     if (c->stream) hipStreamSynchronize(c->stream);
+    if (c->ustream) hipStreamSynchronize(c->ustream);
     for (auto e : c->ev) hipEventDestroy(e);
     for (auto e : c->evb)
         if (e) hipEventDestroy(e);
@@ -154,15 +179,20 @@ extern "C" int mp2vg_destroy(mp2vg_ctx_t* c) {
         if (e) hipEventDestroy(e);
 
     hipFree(c->d_pool);
-    hipFree(c->d_pics);
-    hipFree(c->d_mbs);
-    hipFree(c->d_coefs);
-    hipFree(c->d_slices);
+    for (Bank& b : c->bank) {
+        hipFree(b.d_pics);
+        hipFree(b.d_mbs);
+        hipFree(b.d_coefs);
+        hipFree(b.d_slices);
+        if (b.uploaded) hipEventDestroy(b.uploaded);
+        if (b.consumed) hipEventDestroy(b.consumed);
+    }
     hipFree(c->d_dslots);
     hipFree(c->d_digest);
     if (c->h_stage) hipHostFree(c->h_stage);
     for (auto e : c->sev) hipEventDestroy(e);
     for (auto st : c->sstreams) hipStreamDestroy(st);
+    if (c->ustream) hipStreamDestroy(c->ustream);
     if (c->stream) hipStreamDestroy(c->stream);
     delete c;
     return MP2VG_OK;
@@ -236,20 +266,7 @@ static int plan_batch(mp2vg_ctx_t* c, const mp2vg_picture_t* pics, int32_t npics
         uses_of[2 * (size_t)p + 1] = uses[1];
         return nullptr;
     };
-    {
-        const int nth = std::max(1, std::min({npics, 16, (int)std::thread::hardware_concurrency()}));
-        std::atomic<int> next(0);
-        auto worker = [&]() {
-            for (int p; (p = next.fetch_add(1)) < npics;) err[p] = validate(p);
-        };
-        if (nth == 1) {
-            worker();
-        } else {
-            std::vector<std::thread> th;
-            for (int t = 0; t < nth; t++) th.emplace_back(worker);
-            for (auto& t : th) t.join();
-        }
-    }
+    parallel_for(npics, 16, [&](int p) { err[p] = validate(p); });
     for (int p = 0; p < npics; p++) {
         const mp2vg_picture_t& P = pics[p];
         if (err[p]) {
@@ -360,31 +377,67 @@ static int plan_batch(mp2vg_ctx_t* c, const mp2vg_picture_t* pics, int32_t npics
     return MP2VG_OK;
 }
 
-extern "C" int mp2vg_batch_upload(mp2vg_ctx_t* c, const mp2vg_picture_t* pics, int32_t npics,
-                                  const mp2vg_mb_t* mbs, uint64_t nmbs, const uint32_t* coefs,
-                                  uint64_t ncoefs) {
+static int batch_upload(mp2vg_ctx_t* c, const mp2vg_picture_t* pics, int32_t npics, const mp2vg_mb_t* mbs,
+                        uint64_t nmbs, const uint32_t* coefs, uint64_t ncoefs, bool pinned, bool async) {
     if (!c || !pics || npics <= 0 || !mbs || (!coefs && ncoefs)) return MP2VG_E_INVALID;
     HIPCHK(hipSetDevice(c->cfg.device));
     c->batch_ready = false;
     std::vector<SliceDesc> slices;
     std::vector<Launch> lb;
+    double tp = now_ms();
     int rc = plan_batch(c, pics, npics, mbs, nmbs, coefs, ncoefs, slices, lb);
     if (rc != MP2VG_OK) return rc;
-    HIPCHK(hipStreamSynchronize(c->stream));
-    if ((rc = grow(c->d_pics, c->cap_pics, (size_t)npics)) != MP2VG_OK) return rc;
-    if ((rc = grow(c->d_mbs, c->cap_mbs, (size_t)nmbs + kMbPad)) != MP2VG_OK) return rc;
+    tp = trace_phase("upload: plan", tp);
+    // the other bank from the last upload; the decode queued on it is still allowed to run
+    const int k = (c->cur + 1) & 1;
+    Bank& b = c->bank[k];
+    if (b.decoded) HIPCHK(hipEventSynchronize(b.consumed));
+    if ((rc = grow(b.d_pics, b.cap_pics, (size_t)npics)) != MP2VG_OK) return rc;
+    if ((rc = grow(b.d_mbs, b.cap_mbs, (size_t)nmbs + kMbPad)) != MP2VG_OK) return rc;
     // the kernel loads 128 words from the first coefficient of each MB group unconditionally
-    if ((rc = grow(c->d_coefs, c->cap_coefs, (size_t)ncoefs + kCoefPad)) != MP2VG_OK) return rc;
-    if ((rc = grow(c->d_slices, c->cap_slices, slices.size())) != MP2VG_OK) return rc;
-    if ((rc = upload(c, c->d_pics, pics, sizeof(mp2vg_picture_t) * npics)) != MP2VG_OK) return rc;
-    if ((rc = upload(c, c->d_mbs, mbs, sizeof(mp2vg_mb_t) * nmbs)) != MP2VG_OK) return rc;
-    if (ncoefs && (rc = upload(c, c->d_coefs, coefs, sizeof(uint32_t) * ncoefs)) != MP2VG_OK) return rc;
-    if ((rc = upload(c, c->d_slices, slices.data(), sizeof(SliceDesc) * slices.size())) != MP2VG_OK) return rc;
-    c->launches = lb;
-    c->batch_pics = npics;
+    if ((rc = grow(b.d_coefs, b.cap_coefs, (size_t)ncoefs + kCoefPad)) != MP2VG_OK) return rc;
+    if ((rc = grow(b.d_slices, b.cap_slices, slices.size())) != MP2VG_OK) return rc;
+    // picture records (small, may sit in pageable memory either way) and this function's own
+    // slice descriptors go through staging first: the staged copies end synchronised
+    if ((rc = upload(c, b.d_pics, pics, sizeof(mp2vg_picture_t) * npics, false)) != MP2VG_OK) return rc;
+    if ((rc = upload(c, b.d_slices, slices.data(), sizeof(SliceDesc) * slices.size(), false)) != MP2VG_OK)
+        return rc;
+    if ((rc = upload(c, b.d_mbs, mbs, sizeof(mp2vg_mb_t) * nmbs, pinned)) != MP2VG_OK) return rc;
+    if (ncoefs && (rc = upload(c, b.d_coefs, coefs, sizeof(uint32_t) * ncoefs, pinned)) != MP2VG_OK) return rc;
+    HIPCHK(hipEventRecord(b.uploaded, c->ustream));
+    // the caller's host buffers are free again, unless it asked for an asynchronous upload of
+    // pinned buffers (it then waits with ctx_wait_upload before rewriting them)
+    if (!async) HIPCHK(hipStreamSynchronize(c->ustream));
+    trace_phase("upload: copy", tp);
+    b.launches = std::move(lb);
+    b.npics = npics;
+    c->cur = k;
     c->batch_ready = true;
     return MP2VG_OK;
 }
+
+extern "C" int mp2vg_batch_upload(mp2vg_ctx_t* c, const mp2vg_picture_t* pics, int32_t npics,
+                                  const mp2vg_mb_t* mbs, uint64_t nmbs, const uint32_t* coefs,
+                                  uint64_t ncoefs) {
+    return batch_upload(c, pics, npics, mbs, nmbs, coefs, ncoefs, false, false);
+}
+
+namespace mp2vg {
+// Drop-in decoder (decoder.cpp): records in pinned host memory go to the device without staging
+// and without waiting for the copies.  Its pinned buffer set i feeds bank i (banks alternate per
+// upload): before rewriting set ctx_next_bank(), it calls ctx_wait_upload(ctx, that bank).
+int batch_upload_pinned(mp2vg_ctx_t* c, const mp2vg_picture_t* pics, int32_t npics, const mp2vg_mb_t* mbs,
+                        uint64_t nmbs, const uint32_t* coefs, uint64_t ncoefs) {
+    return batch_upload(c, pics, npics, mbs, nmbs, coefs, ncoefs, true, true);
+}
+int ctx_next_bank(const mp2vg_ctx_t* c) { return (c->cur + 1) & 1; }
+int ctx_wait_upload(mp2vg_ctx_t* c, int bank) {
+    HIPCHK(hipEventSynchronize(c->bank[bank].uploaded));
+    return MP2VG_OK;
+}
+hipStream_t ctx_stream(mp2vg_ctx_t* c) { return c->stream; }
+void ctx_set_launch_timing(mp2vg_ctx_t* c, bool on) { c->launch_timing = on; }
+}  // namespace mp2vg
 
 extern "C" int mp2vg_batch_decode(mp2vg_ctx_t* c) {
     if (!c) return MP2VG_E_INVALID;
@@ -393,7 +446,9 @@ extern "C" int mp2vg_batch_decode(mp2vg_ctx_t* c) {
         return MP2VG_E_STATE;
     }
     HIPCHK(hipSetDevice(c->cfg.device));
-    int nl = (int)c->launches.size();
+    Bank& b = c->bank[c->cur];
+    const std::vector<Launch>& launches = b.launches;
+    int nl = (int)launches.size();
     while ((int)c->ev.size() < 2 * nl) {
         hipEvent_t e;
         HIPCHK(hipEventCreate(&e));
@@ -402,10 +457,10 @@ extern "C" int mp2vg_batch_decode(mp2vg_ctx_t* c) {
 
     KArgs a;
     memset(&a, 0, sizeof a);
-    a.pics = c->d_pics;
-    a.mbs = c->d_mbs;
-    a.coefs = c->d_coefs;
-    a.slices = c->d_slices;
+    a.pics = b.d_pics;
+    a.mbs = b.d_mbs;
+    a.coefs = b.d_coefs;
+    a.slices = b.d_slices;
     a.pool = c->d_pool;
     a.sink = c->d_pool + (size_t)c->g.slot_bytes * c->nslots + kSinkOff;
     a.slot_bytes = c->g.slot_bytes;
@@ -418,7 +473,7 @@ extern "C" int mp2vg_batch_decode(mp2vg_ctx_t* c) {
     // start after everything queued before this batch (evb[0]) and set 0's stream waits for all
     // of them at the end, so API calls that synchronise on c->stream see the whole batch.
     int nsets = 1;
-    for (const Launch& L : c->launches) nsets = std::max(nsets, L.set + 1);
+    for (const Launch& L : launches) nsets = std::max(nsets, L.set + 1);
     while ((int)c->sstreams.size() < nsets - 1) {
         hipStream_t st;
         hipEvent_t e;
@@ -428,22 +483,25 @@ extern "C" int mp2vg_batch_decode(mp2vg_ctx_t* c) {
         c->sev.push_back(e);
     }
     auto stream_of = [&](int set) { return set == 0 ? c->stream : c->sstreams[set - 1]; };
+    HIPCHK(hipStreamWaitEvent(c->stream, b.uploaded, 0));
     HIPCHK(hipEventRecord(c->evb[0], c->stream));
     for (int set = 1; set < nsets; set++) HIPCHK(hipStreamWaitEvent(stream_of(set), c->evb[0], 0));
     for (int i = 0; i < nl; i++) {
-        const hipStream_t st = stream_of(c->launches[i].set);
-        a.slice_base = c->launches[i].begin;
-        a.nslices = c->launches[i].end - c->launches[i].begin;
-        HIPCHK(hipEventRecord(c->ev[2 * i], st));
-        if (a.nslices) HIPCHK(launch_recon(c->g.cf, c->launches[i].mcm, a, st));
-        HIPCHK(hipEventRecord(c->ev[2 * i + 1], st));
+        const hipStream_t st = stream_of(launches[i].set);
+        a.slice_base = launches[i].begin;
+        a.nslices = launches[i].end - launches[i].begin;
+        if (c->launch_timing) HIPCHK(hipEventRecord(c->ev[2 * i], st));
+        if (a.nslices) HIPCHK(launch_recon(c->g.cf, launches[i].mcm, a, st));
+        if (c->launch_timing) HIPCHK(hipEventRecord(c->ev[2 * i + 1], st));
     }
     for (int set = 1; set < nsets; set++) {
         HIPCHK(hipEventRecord(c->sev[set - 1], stream_of(set)));
         HIPCHK(hipStreamWaitEvent(c->stream, c->sev[set - 1], 0));
     }
     HIPCHK(hipEventRecord(c->evb[1], c->stream));
-    c->nlaunch = nl;
+    HIPCHK(hipEventRecord(b.consumed, c->stream));
+    b.decoded = true;
+    c->nlaunch = c->launch_timing ? nl : 0;
     return MP2VG_OK;
 }
 

@@ -5,6 +5,7 @@
 #pragma once
 #include <cstdint>
 #include <cstring>
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -68,6 +69,13 @@ struct BitReader {
         if (n) skip(n);
         return v;
     }
+    // No-refill variants for a caller that has just refilled (>= 33 valid bits) and consumes at
+    // most that many before the next refill: the DCT coefficient loop does one refill per code.
+    inline uint32_t peek_nr(int n) const { return (uint32_t)(cache >> (64 - n)); }  // 1 <= n <= 32
+    inline void skip_nr(int n) {
+        cache <<= n;
+        bits -= n;
+    }
     uint64_t bitpos() const { return (uint64_t)(p - base) * 8 - bits; }
     bool overrun() const { return p > end + 8; }
 };
@@ -129,29 +137,42 @@ struct VlcLut {
     }
 };
 
-// DCT coefficient decoder (B.14 / B.15) with the sign bit folded in: one 10-bit lookup decodes
-// the common short codes completely; longer codes take a second 7-bit lookup.
+// DCT coefficient decoder (B.14 / B.15) with the sign bit folded in: one 12-bit lookup decodes
+// the common codes completely (sign included); longer codes (up to 16 + sign bits) take a second
+// 5-bit lookup.  The escape (6-bit code, 6-bit run, signed 12-bit level) is decoded without a
+// branch: it is frequent in noisy content (9 % of the codes of the bench stream) and a branch on
+// it mispredicts.
 // Entry: bits 0-4 bits consumed (0 = invalid), 5-10 run, 11-22 signed level, 23-24 kind.
 struct CoefLut {
-    enum { NORMAL = 0, EOB = 1, ESC = 2, SUB = 3, L1 = 10, L2 = 7 };
-    std::vector<uint32_t> l1, l2;  // l2: 128-entry sub-tables
+    enum { NORMAL = 0, EOB = 1, ESC = 2, SUB = 3, L1 = 12, L2 = 5 };
+    std::vector<uint32_t> l1, l2;  // l2: (1 << L2)-entry sub-tables
     static uint32_t pack(int len, int run, int level, int kind) {
         return (uint32_t)len | ((uint32_t)run << 5) | (((uint32_t)level & 0xfff) << 11) | ((uint32_t)kind << 23);
     }
     // code: '0'/'1' string; sign appended for NORMAL codes
     void add(const char* bits, int run, int level, int kind);
-    // returns kind; run / level / consumes the code (and the sign bit)
+    // returns NORMAL (escapes included), EOB or -1; run / level; consumes the code (and the sign
+    // bit, or the escape's run and level)
     inline int decode(BitReader& br, int& run, int& level) const {
-        uint32_t e = l1[br.peek(L1)];
-        if (((e >> 23) & 3) == SUB) {
-            br.skip(L1);
-            e = l2[((e >> 5) & 0x3ffff) * 128 + br.peek(L2)];
+        br.refill();  // >= 33 bits: the longest code plus the escape's run and level is 24
+        return decode_nr(br, run, level);
+    }
+    // after a refill; consumes at most 24 bits
+    inline int decode_nr(BitReader& br, int& run, int& level) const {
+        uint32_t e = l1[br.peek_nr(L1)];
+        if (__builtin_expect(((e >> 23) & 3) == SUB, 0)) {
+            br.skip_nr(L1);
+            e = l2[(((e >> 5) & 0x3ffff) << L2) + br.peek_nr(L2)];
         }
-        if (!(e & 31)) return -1;
-        br.skip((int)(e & 31));
-        run = (int)((e >> 5) & 63);
-        level = (int)((int32_t)(e << 9) >> 20);  // sign-extend bits 11-22
-        return (int)((e >> 23) & 3);
+        const int len = (int)(e & 31);
+        if (__builtin_expect(!len, 0)) return -1;
+        const int kind = (int)((e >> 23) & 3);
+        const bool esc = kind == ESC;                             // the escape code is 6 bits
+        const uint32_t x = (uint32_t)((br.cache << 6) >> 46);     // the 18 bits after it
+        run = esc ? (int)(x >> 12) : (int)((e >> 5) & 63);
+        level = esc ? ((int32_t)(x << 20) >> 20) : (int)((int32_t)(e << 9) >> 20);  // signed 12 bits
+        br.skip_nr(len + (esc ? 18 : 0));
+        return esc ? (int)NORMAL : kind;
     }
 };
 
@@ -270,6 +291,10 @@ inline bool mc_reads_inside(const Geom& g, int mbx, int mby, int mvx, int mvy, b
 
 void set_error(const std::string& msg);
 
+// fn(0) .. fn(n-1) on the calling thread plus up to max_threads - 1 persistent helper threads;
+// returns when all calls have returned (tables.cpp)
+void parallel_for(int n, int max_threads, const std::function<void(int)>& fn);
+
 // Host phase timing for diagnosis: with MP2VG_TRACE set, trace_phase(name, t0) prints the
 // milliseconds since t0 to stderr and returns the current time.
 double now_ms();
@@ -287,5 +312,6 @@ int parse_session_npics(const ParseSession* s);
 const mp2vg_picture_t* parse_session_pictures(const ParseSession* s);  // dst_slot = decode index
 const int32_t* parse_session_display(const ParseSession* s);           // npics entries
 int parse_session_wait(ParseSession* s, int p);  // status of picture p once its slices are parsed
-void parse_session_append(ParseSession* s, int p, mp2vg_mb_t* mbs_out, std::vector<uint32_t>& coefs);
+size_t parse_session_ncoefs(const ParseSession* s, int p);  // after parse_session_wait
+void parse_session_append(ParseSession* s, int p, mp2vg_mb_t* mbs_out, uint32_t* coefs_out, uint32_t base);
 void parse_session_free(ParseSession* s);

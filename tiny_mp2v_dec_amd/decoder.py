@@ -79,7 +79,10 @@ class mp2v_decoder_c:  # noqa: N801  (reference name)
     def decode(self, buffer, length=None):
         data = bytes(buffer) if not isinstance(buffer, (bytes, bytearray)) else buffer
         n = len(data) if length is None else int(length)
-        buf = np.frombuffer(bytes(data[:n]) + b"\0" * 64, dtype=np.uint8)
+        if n > len(data):
+            raise ValueError("length exceeds the buffer")
+        # no copy: the parser reads exactly [0, n) (zeros past the end, syntax.h BitReader)
+        buf = np.frombuffer(data, dtype=np.uint8, count=n)
         check(lib().mp2vg_decoder_decode(self._h, buf.ctypes.data_as(ctypes.c_void_p), n), "decoder_decode")
         if self._error is not None:
             e, self._error = self._error, None

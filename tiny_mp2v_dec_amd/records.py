@@ -46,7 +46,7 @@ class Parsed:
     def __init__(self, es: bytes, width, height, chroma_format, threads=0, reordering=True):
         self.width, self.height, self.chroma_format = width, height, chroma_format
         cfg = _lib.make_config(width, height, chroma_format, threads=threads, reordering=reordering)
-        buf = np.frombuffer(es + b"\0" * 64, dtype=np.uint8)
+        buf = np.frombuffer(es, dtype=np.uint8)
         h = ctypes.c_void_p()
         check(lib().mp2vg_parse_es(buf.ctypes.data_as(ctypes.c_void_p), len(es), ctypes.byref(cfg),
                                    ctypes.byref(h)), "parse_es")

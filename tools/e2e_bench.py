@@ -9,6 +9,7 @@ Stages timed on one stream (seed 1729):
   download  D2H of every decoded frame into host planes (frame_c layout)
   dropin    mp2v_decoder_c.decode(): parse + chunked upload/decode/download + display-order
             render callbacks, i.e. what a caller of the reference API sees
+  reference (--ref) the real reference decoder on the same stream and host (bench.cpu_baseline)
 Prints one JSON line.  DESIGN.md quotes these as the PCIe-inclusive rates (never `value`).
 """
 import argparse
@@ -32,6 +33,8 @@ def main():
     ap.add_argument("--gops", type=int, default=16)
     ap.add_argument("--config", default="c2", choices=sorted(bench.CONFIGS))
     ap.add_argument("--threads", type=int, default=min(16, os.cpu_count() or 1))
+    ap.add_argument("--ref", action="store_true", help="also time the real reference (oracle/_ref/ref_decode) "
+                    "on the same stream and host")
     a = ap.parse_args()
     w, h, cf, extra, desc = bench.CONFIGS[a.config]
     es = R.generate_es(width=w, height=h, chroma_format=cf, n_gops=a.gops, seed=1729, **extra)
@@ -83,6 +86,11 @@ def main():
         "dropin_fps": round(n / t_drop, 1),
         "pcie_inclusive_fps": round(n / (t_up + t_dev + t_down), 1),
     }
+    if a.ref:
+        cb = bench.cpu_baseline(es, w, h, cf, n)
+        out["reference_fps"] = cb["value"]
+        out["reference_threads"] = cb["cores"]
+        out["reference_fps_1thread"] = cb.get("value_1thread")
     print(json.dumps(out), flush=True)
 
 
