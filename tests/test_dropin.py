@@ -60,3 +60,23 @@ def test_dropin_long_stream_recycles_slots():
     dec.decode(es)
     dec.close()
     assert got == exp
+
+
+def test_dropin_decoder_reused_across_streams():
+    """One decoder, consecutive decode() calls: the persistent pinned frame pool, the two pinned
+    record sets and the two device record banks carry over between calls (decoder.cpp,
+    runtime.cpp), and every call still renders the oracle's frames in display order."""
+    from helpers import oracle_frames, yuv_md5
+    from tiny_mp2v_dec_amd.records import Parsed, generate_es
+    streams = [generate_es(width=176, height=144, chroma_format=1, n_gops=n, gop_n=12, gop_m=3, seed=s)
+               for n, s in ((5, 41), (2, 42), (7, 43))]
+    got = []
+    dec = mp2v_decoder_c(decoder_config_t(176, 144, 1, pictures_pool_size=4, num_threads=3),
+                         lambda f: got.append(hashlib.md5(f.yuv_bytes()).hexdigest()))
+    for es in streams:
+        parsed = Parsed(es, 176, 144, 1)
+        exp = [yuv_md5(oracle_frames(parsed)[d]) for d in parsed.display]
+        got.clear()
+        dec.decode(es)
+        assert got == exp
+    dec.close()
