@@ -198,7 +198,7 @@ extern "C" int mp2vg_decoder_decode(mp2vg_decoder_t* d, const uint8_t* buf, uint
     ParseSession* ps = nullptr;
     const int threads = d->cfg.num_threads > 0 ? d->cfg.num_threads : (int)std::thread::hardware_concurrency();
     // (16-thread box: 2 or 4 threads kept back 1,975 frames/s, 1 -> 1,864, 6 -> 1,661)
-    int rc = parse_session_start(buf, len, &d->cfg, std::max(1, threads - 2), &ps);
+    int rc = parse_session_start(buf, len, &d->cfg, std::max(1, threads - 2), 4 * kChunk, &ps);
     t0 = trace_phase("dropin: headers", t0);
     if (rc != MP2VG_OK) return rc;
     std::unique_ptr<ParseSession, void (*)(ParseSession*)> guard(ps, parse_session_free);

@@ -436,24 +436,54 @@ struct ParseSession {
     std::atomic<int> next_pic{0};
     std::vector<std::thread> workers;
     size_t mbs_per_pic = 0;
+    // Streaming (window > 0, the drop-in decoder): a worker parses picture p only once
+    // p < consumed + window, into a per-picture MB record buffer that parse_session_append
+    // recycles, so host memory stays O(window) for any stream length.  window == 0
+    // (mp2vg_parse_es): every picture's records go to res->mbs.
+    int window = 0;
+    int consumed = 0;  // pictures appended (under mu)
+    bool stop = false;  // the consumer is gone: waiting workers return
+    std::vector<mp2vg_mb_t*> pic_mbs;  // streaming: picture -> its buffer while parsed, not appended
+    std::vector<mp2vg_mb_t*> spare;    // streaming: recycled buffers
 
     ~ParseSession() {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            stop = true;
+        }
+        cv.notify_all();
         join();
+        for (mp2vg_mb_t* b : pic_mbs) delete[] b;
+        for (mp2vg_mb_t* b : spare) delete[] b;
         delete res;
     }
     void join() {
         for (auto& t : workers) t.join();
         workers.clear();
     }
+    mp2vg_mb_t* mbs_of(int p) { return window ? pic_mbs[p] : res->mbs.data() + mbs_per_pic * p; }
     void work() {
         const int npics = (int)C.pics.size();
         for (;;) {
             const int p = next_pic.fetch_add(1);
             if (p >= npics) return;
+            if (window) {
+                mp2vg_mb_t* b = nullptr;
+                {
+                    std::unique_lock<std::mutex> lk(mu);
+                    cv.wait(lk, [&] { return stop || p < consumed + window; });
+                    if (stop) return;
+                    if (!spare.empty()) {
+                        b = spare.back();
+                        spare.pop_back();
+                    }
+                }
+                pic_mbs[p] = b ? b : new mp2vg_mb_t[mbs_per_pic];  // every record is written by its slice
+            }
             int st = MP2VG_OK;
             std::string msg;
             for (size_t j = pic_job_begin[p]; j < pic_job_begin[p + 1]; j++) {
-                parse_slice(C, C.pics[p], jobs[j], res->mbs.data() + mbs_per_pic * p, row_done[p], outs[j]);
+                parse_slice(C, C.pics[p], jobs[j], mbs_of(p), row_done[p], outs[j]);
                 if (outs[j].status != MP2VG_OK && st == MP2VG_OK) {
                     char m[256];
                     snprintf(m, sizeof m, "picture %d slice @%llu: %s", p, (unsigned long long)jobs[j].byte_off,
@@ -485,7 +515,7 @@ struct ParseSession {
     }
 };
 
-int parse_session_start(const uint8_t* buf, uint64_t len, const mp2vg_config_t* cfg, int threads,
+int parse_session_start(const uint8_t* buf, uint64_t len, const mp2vg_config_t* cfg, int threads, int window,
                         ParseSession** out) {
     if (!buf || !cfg || !out) return MP2VG_E_INVALID;
     *out = nullptr;
@@ -627,7 +657,11 @@ int parse_session_start(const uint8_t* buf, uint64_t len, const mp2vg_config_t* 
     S->mbs_per_pic = mbs_per_pic;
     auto* res = new mp2vg_parsed();
     S->res = res;
-    res->mbs.resize(mbs_per_pic * npics);
+    S->window = std::max(0, window);
+    if (S->window)
+        S->pic_mbs.assign(npics, nullptr);
+    else
+        res->mbs.resize(mbs_per_pic * npics);
     for (auto& P : C.pics)
         for (auto& j : P.slices) S->jobs.push_back(j);
     S->outs.resize(S->jobs.size());
@@ -700,7 +734,7 @@ size_t parse_session_ncoefs(const ParseSession* s, int p) {
 // `base` of the caller's batch).  The picture's parse buffers are released.
 void parse_session_append(ParseSession* s, int p, mp2vg_mb_t* mbs_out, uint32_t* coefs_out, uint32_t base) {
     const size_t n = s->mbs_per_pic;
-    memcpy(mbs_out, s->res->mbs.data() + n * p, n * sizeof(mp2vg_mb_t));
+    memcpy(mbs_out, s->mbs_of(p), n * sizeof(mp2vg_mb_t));
     for (size_t j = s->pic_job_begin[p]; j < s->pic_job_begin[p + 1]; j++) {
         SliceOut& o = s->outs[j];
         if (!o.coefs.empty()) memcpy(coefs_out, o.coefs.data(), o.coefs.size() * 4);
@@ -710,6 +744,15 @@ void parse_session_append(ParseSession* s, int p, mp2vg_mb_t* mbs_out, uint32_t*
         base += (uint32_t)o.coefs.size();
         CoefVec().swap(o.coefs);
     }
+    if (s->window) {
+        {
+            std::lock_guard<std::mutex> lk(s->mu);
+            s->spare.push_back(s->pic_mbs[p]);
+            s->pic_mbs[p] = nullptr;
+            s->consumed++;
+        }
+        s->cv.notify_all();
+    }
 }
 
 extern "C" int mp2vg_parse_es(const uint8_t* buf, uint64_t len, const mp2vg_config_t* cfg,
@@ -717,7 +760,7 @@ extern "C" int mp2vg_parse_es(const uint8_t* buf, uint64_t len, const mp2vg_conf
     if (!out) return MP2VG_E_INVALID;
     *out = nullptr;
     ParseSession* sp = nullptr;
-    int rc = parse_session_start(buf, len, cfg, cfg ? cfg->num_threads : 0, &sp);
+    int rc = parse_session_start(buf, len, cfg, cfg ? cfg->num_threads : 0, 0, &sp);
     if (rc != MP2VG_OK) return rc;
     std::unique_ptr<ParseSession> S(sp);
     double tp = now_ms();

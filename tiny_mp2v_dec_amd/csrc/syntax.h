@@ -306,7 +306,8 @@ double trace_phase(const char* name, double t0);
 // the calling thread, pass 2 (slices -> MB records + coefficient words) on `threads` workers that
 // publish pictures in about decode order.  mp2vg_parse_es and the drop-in decoder both use it.
 struct ParseSession;
-int parse_session_start(const uint8_t* buf, uint64_t len, const mp2vg_config_t* cfg, int threads,
+// window > 0: parse at most `window` pictures ahead of parse_session_append (bounded host memory)
+int parse_session_start(const uint8_t* buf, uint64_t len, const mp2vg_config_t* cfg, int threads, int window,
                         ParseSession** out);
 int parse_session_npics(const ParseSession* s);
 const mp2vg_picture_t* parse_session_pictures(const ParseSession* s);  // dst_slot = decode index
