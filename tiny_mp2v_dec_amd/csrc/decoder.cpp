@@ -40,6 +40,10 @@ void ctx_set_launch_timing(mp2vg_ctx_t* c, bool on);
 namespace {
 // pictures per device batch (MP2VG_CHUNK overrides it for measurements)
 const int kChunk = getenv("MP2VG_CHUNK") ? std::max(1, atoi(getenv("MP2VG_CHUNK"))) : 16;
+// frame download streams (768-frame c2 e2e: 1 stream 6,925-7,124 frames/s, 2: 6,904-6,949, 4:
+// 7,451-7,488; MP2VG_DL_STREAMS overrides it for measurements)
+constexpr int kMaxDl = 4;
+const int kDlStreams = getenv("MP2VG_DL_STREAMS") ? std::min(kMaxDl, std::max(1, atoi(getenv("MP2VG_DL_STREAMS")))) : 4;
 
 // Host frames live in pinned memory, in the device slot layout (= the reference frame_c layout),
 // so a decoded slot comes back with one contiguous DMA copy.  They are recycled after the render
@@ -132,17 +136,21 @@ struct mp2vg_decoder {
     int nslots = 0;
     std::unique_ptr<FramePool> pool;
     PinnedBuf mbuf[2], cbuf[2];        // chunk MB records / coefficient words, one set per record bank
-    hipStream_t dl = nullptr;          // frame downloads
+    // frame downloads, slots dealt round-robin: each stream's copies go to their own DMA engine
+    hipStream_t dl[kMaxDl] = {};
+    int ndl = 1;
     hipEvent_t decoded = nullptr;      // end of the last chunk's decode (on the context stream)
 };
 
 extern "C" int mp2vg_decoder_destroy(mp2vg_decoder_t* d) {
     if (!d) return MP2VG_E_INVALID;
-    if (d->dl) hipStreamSynchronize(d->dl);
+    for (hipStream_t st : d->dl)
+        if (st) hipStreamSynchronize(st);
     if (d->ctx) mp2vg_synchronize(d->ctx);
     d->pool.reset();
     if (d->decoded) hipEventDestroy(d->decoded);
-    if (d->dl) hipStreamDestroy(d->dl);
+    for (hipStream_t st : d->dl)
+        if (st) hipStreamDestroy(st);
     if (d->ctx) mp2vg_destroy(d->ctx);
     delete d;
     return MP2VG_OK;
@@ -167,7 +175,10 @@ extern "C" int mp2vg_decoder_create(const mp2vg_config_t* cfg, mp2vg_render_fn f
     d->nslots = c.pictures_pool_size;
     d->pool.reset(new FramePool(d->g.slot_bytes));
     ctx_set_launch_timing(ctx, false);  // no per-launch events on the drop-in's chunk path
-    if (hipStreamCreateWithFlags(&d->dl, hipStreamNonBlocking) != hipSuccess ||
+    d->ndl = kDlStreams;
+    bool sok = true;
+    for (int i = 0; i < d->ndl; i++) sok = sok && hipStreamCreateWithFlags(&d->dl[i], hipStreamNonBlocking) == hipSuccess;
+    if (!sok ||
         hipEventCreateWithFlags(&d->decoded, hipEventDisableTiming) != hipSuccess) {
         set_error("download stream / event creation failed");
         mp2vg_decoder_destroy(d);
@@ -219,7 +230,6 @@ extern "C" int mp2vg_decoder_decode(mp2vg_decoder_t* d, const uint8_t* buf, uint
     std::deque<HostFrame*> q;
     bool done = false;
     FramePool& pool = *d->pool;
-    hipStream_t dl = d->dl;
     std::thread render([&]() {
         for (;;) {
             HostFrame* f;
@@ -246,7 +256,7 @@ extern "C" int mp2vg_decoder_decode(mp2vg_decoder_t* d, const uint8_t* buf, uint
     const uint64_t mbs_per_pic = (uint64_t)(d->cfg.width / 16) * (d->cfg.height / 16);
 
     auto finish = [&](int status) {
-        hipStreamSynchronize(dl);  // no copy may still target a pool frame
+        for (int i = 0; i < d->ndl; i++) hipStreamSynchronize(d->dl[i]);  // no copy may still target a pool frame
         mp2vg_synchronize(d->ctx);
         {
             std::lock_guard<std::mutex> lk(mu);
@@ -270,7 +280,8 @@ extern "C" int mp2vg_decoder_decode(mp2vg_decoder_t* d, const uint8_t* buf, uint
     auto complete_pending = [&]() -> int {
         if (pend_e < 0) return MP2VG_OK;
         tc = now_ms();
-        if (hipStreamSynchronize(dl) != hipSuccess) return MP2VG_E_HIP;
+        for (int i = 0; i < d->ndl; i++)
+            if (hipStreamSynchronize(d->dl[i]) != hipSuccess) return MP2VG_E_HIP;
         t_down += now_ms() - tc;
         for (auto& kv : inflight) ready[kv.first] = kv.second;
         inflight.clear();
@@ -347,7 +358,8 @@ extern "C" int mp2vg_decoder_decode(mp2vg_decoder_t* d, const uint8_t* buf, uint
         decoded_e = e;
         if ((rc = complete_pending()) != MP2VG_OK) return finish(rc);
         // copies of this chunk into frame_c-layout host frames, one DMA per slot, after its decode
-        if (hipStreamWaitEvent(dl, d->decoded, 0) != hipSuccess) return finish(MP2VG_E_HIP);
+        for (int i = 0; i < d->ndl; i++)
+            if (hipStreamWaitEvent(d->dl[i], d->decoded, 0) != hipSuccess) return finish(MP2VG_E_HIP);
         for (int p = s; p < e; p++) {
             HostFrame* hf = pool.get();
             if (!hf) return finish(MP2VG_E_NOMEM);
@@ -361,7 +373,7 @@ extern "C" int mp2vg_decoder_decode(mp2vg_decoder_t* d, const uint8_t* buf, uint
             hf->f.decode_index = p;
             void* src = nullptr;
             rc = mp2vg_slot_device_ptr(d->ctx, slot_of[p], &src);
-            if (rc == MP2VG_OK && hipMemcpyAsync(hf->data, src, d->g.slot_bytes, hipMemcpyDeviceToHost, dl) != hipSuccess)
+            if (rc == MP2VG_OK && hipMemcpyAsync(hf->data, src, d->g.slot_bytes, hipMemcpyDeviceToHost, d->dl[p % d->ndl]) != hipSuccess)
                 rc = MP2VG_E_HIP;
             if (rc != MP2VG_OK) {
                 pool.put(hf);
