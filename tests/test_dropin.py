@@ -80,3 +80,29 @@ def test_dropin_decoder_reused_across_streams():
         dec.decode(es)
         assert got == exp
     dec.close()
+
+
+def test_dropin_bad_stream_fails_cleanly_then_recovers():
+    """A stream that breaks early (picture 2) and one that breaks at its end: decode() reports the
+    error (while parse workers are still ahead of the chunk loop, parse.cpp's window and stop
+    flag), and the same decoder then decodes a good stream to the oracle's frames."""
+    from helpers import oracle_frames, yuv_md5
+    from tiny_mp2v_dec_amd.records import Parsed, generate_es
+    good = generate_es(width=176, height=144, chroma_format=1, n_gops=8, gop_n=12, gop_m=3, seed=51)
+    starts = [i for i in range(len(good) - 4) if good[i:i + 4] == b"\x00\x00\x01\x01"]
+    assert len(starts) > 3
+    early = bytearray(good)
+    early[starts[2] + 8:starts[2] + 40] = bytes(32)  # picture 2, first slice: zeros -> bad MBA code
+    late = good[:starts[-1] + 12]                     # last slice cut short
+    got = []
+    dec = mp2v_decoder_c(decoder_config_t(176, 144, 1, pictures_pool_size=4, num_threads=4),
+                         lambda f: got.append(hashlib.md5(f.yuv_bytes()).hexdigest()))
+    for bad in (bytes(early), late):
+        with pytest.raises(Exception):
+            dec.decode(bad)
+    parsed = Parsed(good, 176, 144, 1)
+    exp = [yuv_md5(oracle_frames(parsed)[d]) for d in parsed.display]
+    got.clear()
+    dec.decode(good)
+    dec.close()
+    assert got == exp
