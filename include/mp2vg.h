@@ -149,6 +149,11 @@ int  mp2vg_synchronize(mp2vg_ctx_t* ctx);
 int  mp2vg_last_launch_times(mp2vg_ctx_t* ctx, float* ms, int32_t max, int32_t* count);
 /* device time (ms) of the whole last mp2vg_batch_decode: first launch start to last launch end */
 int  mp2vg_last_batch_time(mp2vg_ctx_t* ctx, float* ms);
+/* times of the batch decoded `back` decodes ago (0 = the last; the last 64 are kept), so batches
+ * can be decoded back to back and timed afterwards: whole-batch span (batch_ms, may be NULL) and
+ * per-launch device times (launch_ms[0..min(count, max)), may be NULL); synchronises */
+int  mp2vg_batch_times(mp2vg_ctx_t* ctx, int32_t back, float* batch_ms, float* launch_ms, int32_t max,
+                       int32_t* count);
 /* copy one frame slot to host planes (each plane written width x height, tightly packed if
  * dst_stride is 0); synchronous */
 int  mp2vg_download_slot(mp2vg_ctx_t* ctx, int32_t slot, uint8_t* dst_planes[3],

@@ -169,3 +169,30 @@ def test_full_size_1080p_digest_vs_oracle():
             assert all(np.array_equal(got[k], exp[p][k]) for k in range(3))
     host = [R.planes_digest(f) for f in exp[:2]]
     assert [int(x) for x in dig[:2]] == host
+
+
+def test_back_to_back_batches_and_their_timing_events():
+    """Batches decoded back to back without a host sync (as bench.py times them): a re-upload
+    into the other record bank while decodes are queued leaves every frame bit-exact, and every
+    batch's HIP events are readable afterwards (mp2vg_batch_times keeps the last 64)."""
+    from tiny_mp2v_dec_amd.records import generate_es
+    es_a = generate_es(width=176, height=144, chroma_format=1, n_gops=3, gop_n=12, gop_m=3, seed=61)
+    es_b = generate_es(width=176, height=144, chroma_format=1, n_gops=3, gop_n=12, gop_m=3, seed=62)
+    pa, pb = R.Parsed(es_a, 176, 144, 1), R.Parsed(es_b, 176, 144, 1)
+    assert pa.npics == pb.npics
+    with R.DeviceContext(176, 144, 1, slots=pa.npics) as ctx:
+        ctx.upload(pa.pics, pa.mbs, pa.coefs)
+        for _ in range(5):
+            ctx.decode()
+        ctx.upload(pb.pics, pb.mbs, pb.coefs)  # other bank; batch a's decodes may still be queued
+        for _ in range(3):
+            ctx.decode()
+        ctx.synchronize()
+        got = [yuv_md5(ctx.download(int(p["dst_slot"]))) for p in pb.pics]
+        times = [ctx.batch_times(back) for back in range(8)]
+        with pytest.raises(RuntimeError):
+            ctx.batch_times(8)
+    exp = [yuv_md5(f) for f in oracle_frames(pb)]
+    assert got == exp
+    for span, launches in times:
+        assert span > 0 and launches and all(t > 0 for t in launches)

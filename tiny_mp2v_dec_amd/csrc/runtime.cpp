@@ -80,10 +80,17 @@ struct mp2vg_ctx {
     int cur = -1;  // bank of the last upload
     bool batch_ready = false;
 
-    std::vector<hipEvent_t> ev;   // 2 per launch (start, end; on the launch's stream)
-    hipEvent_t evb[2] = {nullptr, nullptr};  // whole batch, main stream
+    // timing events of the last kHist batches (ring, slot = batch sequence number % kHist), so a
+    // caller can decode back to back and read every batch's times afterwards
+    struct BatchEv {
+        hipEvent_t b[2] = {nullptr, nullptr};  // whole batch, main stream
+        std::vector<hipEvent_t> l;             // 2 per launch (start, end; on the launch's stream)
+        int nl = 0;                            // launches timed (0 with launch timing off)
+    };
+    static constexpr int kHist = 64;
+    BatchEv hist[kHist];
+    uint64_t seq = 0;  // batches decoded
     hipEvent_t up_ev[2] = {nullptr, nullptr};  // staging halves of upload()
-    int nlaunch = 0;
     bool launch_timing = true;  // per-launch events (mp2vg_last_launch_times)
 
     void* h_stage = nullptr;
@@ -150,7 +157,6 @@ extern "C" int mp2vg_create(const mp2vg_config_t* cfg, mp2vg_ctx_t** out) {
              hipEventCreateWithFlags(&b.consumed, hipEventDisableTiming) == hipSuccess;
     if (!ok || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->ustream, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreate(&c->evb[0]) != hipSuccess || hipEventCreate(&c->evb[1]) != hipSuccess ||
         hipEventCreateWithFlags(&c->up_ev[0], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->up_ev[1], hipEventDisableTiming) != hipSuccess ||
         hipHostMalloc(&c->h_stage, kStageBytes, hipHostMallocDefault) != hipSuccess) {
@@ -172,9 +178,11 @@ extern "C" int mp2vg_destroy(mp2vg_ctx_t* c) {
     hipSetDevice(c->cfg.device);
     if (c->stream) hipStreamSynchronize(c->stream);
     if (c->ustream) hipStreamSynchronize(c->ustream);
-    for (auto e : c->ev) hipEventDestroy(e);
-    for (auto e : c->evb)
-        if (e) hipEventDestroy(e);
+    for (auto& h : c->hist) {
+        for (auto e : h.l) hipEventDestroy(e);
+        for (auto e : h.b)
+            if (e) hipEventDestroy(e);
+    }
     for (auto e : c->up_ev)
         if (e) hipEventDestroy(e);
 
@@ -449,10 +457,13 @@ extern "C" int mp2vg_batch_decode(mp2vg_ctx_t* c) {
     Bank& b = c->bank[c->cur];
     const std::vector<Launch>& launches = b.launches;
     int nl = (int)launches.size();
-    while ((int)c->ev.size() < 2 * nl) {
+    mp2vg_ctx::BatchEv& H = c->hist[c->seq % mp2vg_ctx::kHist];
+    for (auto& e : H.b)
+        if (!e) HIPCHK(hipEventCreate(&e));
+    while (c->launch_timing && (int)H.l.size() < 2 * nl) {
         hipEvent_t e;
         HIPCHK(hipEventCreate(&e));
-        c->ev.push_back(e);
+        H.l.push_back(e);
     }
 
     KArgs a;
@@ -484,24 +495,25 @@ extern "C" int mp2vg_batch_decode(mp2vg_ctx_t* c) {
     }
     auto stream_of = [&](int set) { return set == 0 ? c->stream : c->sstreams[set - 1]; };
     HIPCHK(hipStreamWaitEvent(c->stream, b.uploaded, 0));
-    HIPCHK(hipEventRecord(c->evb[0], c->stream));
-    for (int set = 1; set < nsets; set++) HIPCHK(hipStreamWaitEvent(stream_of(set), c->evb[0], 0));
+    HIPCHK(hipEventRecord(H.b[0], c->stream));
+    for (int set = 1; set < nsets; set++) HIPCHK(hipStreamWaitEvent(stream_of(set), H.b[0], 0));
     for (int i = 0; i < nl; i++) {
         const hipStream_t st = stream_of(launches[i].set);
         a.slice_base = launches[i].begin;
         a.nslices = launches[i].end - launches[i].begin;
-        if (c->launch_timing) HIPCHK(hipEventRecord(c->ev[2 * i], st));
+        if (c->launch_timing) HIPCHK(hipEventRecord(H.l[2 * i], st));
         if (a.nslices) HIPCHK(launch_recon(c->g.cf, launches[i].mcm, a, st));
-        if (c->launch_timing) HIPCHK(hipEventRecord(c->ev[2 * i + 1], st));
+        if (c->launch_timing) HIPCHK(hipEventRecord(H.l[2 * i + 1], st));
     }
     for (int set = 1; set < nsets; set++) {
         HIPCHK(hipEventRecord(c->sev[set - 1], stream_of(set)));
         HIPCHK(hipStreamWaitEvent(c->stream, c->sev[set - 1], 0));
     }
-    HIPCHK(hipEventRecord(c->evb[1], c->stream));
+    HIPCHK(hipEventRecord(H.b[1], c->stream));
     HIPCHK(hipEventRecord(b.consumed, c->stream));
     b.decoded = true;
-    c->nlaunch = c->launch_timing ? nl : 0;
+    H.nl = c->launch_timing ? nl : 0;
+    c->seq++;
     return MP2VG_OK;
 }
 
@@ -512,25 +524,39 @@ extern "C" int mp2vg_synchronize(mp2vg_ctx_t* c) {
     return MP2VG_OK;
 }
 
-extern "C" int mp2vg_last_launch_times(mp2vg_ctx_t* c, float* ms, int32_t max, int32_t* count) {
-    if (!c) return MP2VG_E_INVALID;
-    HIPCHK(hipSetDevice(c->cfg.device));
-    HIPCHK(hipStreamSynchronize(c->stream));
-    if (count) *count = c->nlaunch;
-    for (int i = 0; i < c->nlaunch && i < max; i++) HIPCHK(hipEventElapsedTime(&ms[i], c->ev[2 * i], c->ev[2 * i + 1]));
-    return MP2VG_OK;
-}
-
-extern "C" int mp2vg_last_batch_time(mp2vg_ctx_t* c, float* ms) {
-    if (!c || !ms) return MP2VG_E_INVALID;
-    if (!c->nlaunch) {
-        set_error("no batch decoded");
+extern "C" int mp2vg_batch_times(mp2vg_ctx_t* c, int32_t back, float* batch_ms, float* launch_ms, int32_t max,
+                                 int32_t* count) {
+    if (!c || back < 0) return MP2VG_E_INVALID;
+    if ((uint64_t)back >= c->seq || back >= mp2vg_ctx::kHist) {
+        set_error("no such decoded batch (mp2vg_batch_times keeps the last 64)");
         return MP2VG_E_STATE;
     }
     HIPCHK(hipSetDevice(c->cfg.device));
     HIPCHK(hipStreamSynchronize(c->stream));
-    HIPCHK(hipEventElapsedTime(ms, c->evb[0], c->evb[1]));
+    const mp2vg_ctx::BatchEv& H = c->hist[(c->seq - 1 - (uint64_t)back) % mp2vg_ctx::kHist];
+    if (batch_ms) HIPCHK(hipEventElapsedTime(batch_ms, H.b[0], H.b[1]));
+    if (count) *count = H.nl;
+    for (int i = 0; launch_ms && i < H.nl && i < max; i++)
+        HIPCHK(hipEventElapsedTime(&launch_ms[i], H.l[2 * i], H.l[2 * i + 1]));
     return MP2VG_OK;
+}
+
+extern "C" int mp2vg_last_launch_times(mp2vg_ctx_t* c, float* ms, int32_t max, int32_t* count) {
+    if (!c) return MP2VG_E_INVALID;
+    if (!c->seq) {
+        if (count) *count = 0;
+        return MP2VG_OK;
+    }
+    return mp2vg_batch_times(c, 0, nullptr, ms, max, count);
+}
+
+extern "C" int mp2vg_last_batch_time(mp2vg_ctx_t* c, float* ms) {
+    if (!c || !ms) return MP2VG_E_INVALID;
+    if (!c->seq) {
+        set_error("no batch decoded");
+        return MP2VG_E_STATE;
+    }
+    return mp2vg_batch_times(c, 0, ms, nullptr, 0, nullptr);
 }
 
 extern "C" int mp2vg_download_slot(mp2vg_ctx_t* c, int32_t slot, uint8_t* dst[3], const int32_t dst_stride[3]) {

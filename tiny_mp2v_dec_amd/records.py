@@ -129,6 +129,15 @@ class DeviceContext:
         check(lib().mp2vg_last_batch_time(self.h, ctypes.byref(ms)), "last_batch_time")
         return ms.value
 
+    def batch_times(self, back=0):
+        """(batch span ms, [per-launch ms]) of the batch decoded `back` decodes ago (0 = last; the
+        last 64 are kept), read from the HIP events recorded when it ran."""
+        ms = ctypes.c_float()
+        buf = (ctypes.c_float * 256)()
+        n = ctypes.c_int32()
+        check(lib().mp2vg_batch_times(self.h, int(back), ctypes.byref(ms), buf, 256, ctypes.byref(n)), "batch_times")
+        return ms.value, list(buf[:min(n.value, 256)])
+
     def download(self, slot):
         """Visible planes of one slot: [Y, U, V] numpy arrays (height x width)."""
         planes = [np.empty((self.ph[i], self.pw[i]), np.uint8) for i in range(3)]
