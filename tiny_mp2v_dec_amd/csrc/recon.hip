@@ -534,6 +534,14 @@ __device__ __forceinline__ uint32_t dq_entry(const Group& S, int lane) {
     return (slot & 0xff) | (pick8(S.qs8, k) << 8) | (wsel << 16) | (intra << 18) | ((uint32_t)coded << 19);
 }
 
+// v_mul_u32_u24 as asm: on a plain product the compiler re-associates the dequant multiply chain
+// into a quarter-rate v_mul_lo_u32
+__device__ __forceinline__ uint32_t mul24_asm(uint32_t a, uint32_t b) {
+    uint32_t r;
+    asm("v_mul_u32_u24 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
 // dequant of one coefficient word (parse_block, mb_decoder.cpp:74-155) into its coded-block
 // slot: lane = word; its MB k (from the word's MB-column bits) and block select the group's
 // dequant entry.  INTRA_ONLY (I pictures: every MB intra, no '1s' first coefficients) drops the
@@ -556,17 +564,20 @@ __device__ __forceinline__ void dequant_word(Lds<CF>& L, int wave, const Group& 
     const int Wi = L.W[(e >> 16) & 3][i];
     const int sign = level < 0 ? -1 : 0;
     const int mag = level < 0 ? -level : level;
+    // W*qs < 2^16 and 2*|level|+1 <= 65537 < 2^24: 24-bit multiplies (full rate) give the low 32
+    // bits of the product, i.e. the reference's int arithmetic, where v_mul_lo_u32 is quarter rate
+    const uint32_t wq = __umul24((uint32_t)Wi, (uint32_t)qs);
     short v;
     int pos;
     if (!INTRA_ONLY && (w & MP2VG_COEF_FIRST1S)) {  // (3*W*qs)>>5 at qfs[0], unclamped (:79-88)
-        const short t = (short)((3 * Wi * qs) >> 5);
+        const short t = (short)((int)(3u * wq) >> 5);
         v = (short)((t ^ sign) - sign);
         pos = 0;
     } else {
-        int val = intra ? (mag * Wi * qs) >> 4 : ((2 * mag + 1) * Wi * qs) >> 5;
+        int val = intra ? (int)mul24_asm((uint32_t)mag, wq) >> 4 : (int)mul24_asm((uint32_t)(2 * mag + 1), wq) >> 5;
         val = (val ^ sign) - sign;
-        const short t = (short)val;  // int16 truncation before the clamp (:146)
-        v = t > 2047 ? (short)2047 : (t < -2048 ? (short)-2048 : t);
+        const int t = (short)val;  // int16 truncation before the clamp (:146)
+        v = (short)min(max(t, -2048), 2047);  // v_med3_i32
         pos = L.scan[i];
     }
     L.blk[wave][slot][pos] = v;
