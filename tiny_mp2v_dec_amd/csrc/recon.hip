@@ -107,6 +107,15 @@ __device__ __forceinline__ void wave_sync() {
 // per-byte (a + b + 1) >> 1 on 4 packed u8 == _mm_avg_epu8: one v_lerp_u8 (rounding bit per byte)
 __device__ __forceinline__ uint32_t avg4(uint32_t a, uint32_t b) { return __builtin_amdgcn_lerp(a, b, 0x01010101u); }
 
+// v_mul_u32_u24 (low 32 bits of a 24 x 24-bit product, full rate) as asm: on plain products the
+// compiler emits quarter-rate v_mul_lo_u32 where it cannot bound an operand (a row index times a
+// runtime stride) or where it re-associates (the dequant W*qs*level chain)
+__device__ __forceinline__ uint32_t mul24_asm(uint32_t a, uint32_t b) {
+    uint32_t r;
+    asm("v_mul_u32_u24 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
 template <int CF>
 struct Fmt {
     static constexpr int NB = CF == 1 ? 6 : (CF == 2 ? 8 : 12);  // blocks per MB
@@ -332,8 +341,8 @@ __device__ __forceinline__ void tap_issue(Tap<NW>& t, bool use, __amdgpu_buffer_
     // dword-aligned row start: byte-exact (unaligned) buffer loads would save two alignbytes per
     // dword but cost twice the texture-address cycles, a net loss (tools/unaligned_check.hip)
     const uint32_t row = plane_off + (uint32_t)(Xc & ~3);
-    const uint32_t o0 = (use && !(ABL & 32)) ? row + (uint32_t)(Y0 * stride) : kNoTap;
-    const uint32_t o1 = (use && hy && edge && !(ABL & 32)) ? row + (uint32_t)(Y1 * stride) : kNoTap;
+    const uint32_t o0 = (use && !(ABL & 32)) ? row + mul24_asm((uint32_t)Y0, (uint32_t)stride) : kNoTap;
+    const uint32_t o1 = (use && hy && edge && !(ABL & 32)) ? row + mul24_asm((uint32_t)Y1, (uint32_t)stride) : kNoTap;
     load_row<NW, ABL>(t.a, ref, o0);
     if (!(ABL & 512)) load_row<NW, ABL>(t.b, ref, o1);  // (dev ablation 512: no edge-row loads)
     else for (int i = 0; i <= NW; i++) t.b[i] = 0;
@@ -482,7 +491,7 @@ __device__ __forceinline__ void store_pass(uint32_t r0, uint32_t r1, bool live, 
     const int pw = plane == 0 ? 16 : F::CW;
     const int phm = plane == 0 ? 16 : F::CH;
     uint8_t* dst = dst_slot + gsel(geo.plane_off, plane) +
-                   (size_t)((int)(r0 >> 16) * phm + py) * gsel(geo.stride, plane) + (int)(r0 & 0xffff) * pw;
+                   mul24_asm((r0 >> 16) * phm + py, (uint32_t)gsel(geo.stride, plane)) + (int)(r0 & 0xffff) * pw;
     dst = live ? dst : wsink;  // branch-free: every lane stores (see Tap)
     if (ABL & 8) {
         asm volatile("" ::"v"(out[0]), "v"(out[1]), "v"(out[2]), "v"(out[3]), "v"(dst));
@@ -532,14 +541,6 @@ __device__ __forceinline__ uint32_t dq_entry(const Group& S, int lane) {
     const uint32_t intra = pick8(S.fl8, k) & MP2VG_MB_INTRA;
     const uint32_t wsel = (bb < 6 ? 0u : 2u) + (intra ? 0u : 1u);
     return (slot & 0xff) | (pick8(S.qs8, k) << 8) | (wsel << 16) | (intra << 18) | ((uint32_t)coded << 19);
-}
-
-// v_mul_u32_u24 as asm: on a plain product the compiler re-associates the dequant multiply chain
-// into a quarter-rate v_mul_lo_u32
-__device__ __forceinline__ uint32_t mul24_asm(uint32_t a, uint32_t b) {
-    uint32_t r;
-    asm("v_mul_u32_u24 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-    return r;
 }
 
 // dequant of one coefficient word (parse_block, mb_decoder.cpp:74-155) into its coded-block
