@@ -196,3 +196,27 @@ def test_back_to_back_batches_and_their_timing_events():
     assert got == exp
     for span, launches in times:
         assert span > 0 and launches and all(t > 0 for t in launches)
+
+
+@pytest.mark.parametrize("config", ["c3", "c4", "c5"])
+def test_bench_config_full_size_every_frame_vs_oracle(config):
+    """The other bench configurations at full size (SURVEY §8d C3 1080p 4:2:2 IPB, C4 4K 4:2:0
+    IPB, C5 1080p 4:4:4 I-only high bitrate): one closed GOP (C5: 4 I pictures) generated exactly
+    as bench.py generates it, every frame's device digest == the digest of the oracle's frame,
+    and the first and last frames compared byte for byte."""
+    import importlib
+    bench = importlib.import_module("bench")
+    width, height, cf, gparams, _ = bench.CONFIGS[config]
+    es = R.generate_es(width=width, height=height, chroma_format=cf, n_gops=4 if config == "c5" else 1,
+                       seed=1729, **gparams)
+    parsed = R.Parsed(es, width, height, cf)
+    exp = oracle_frames(parsed)
+    with R.DeviceContext(width, height, cf, slots=parsed.npics) as ctx:
+        ctx.upload(parsed.pics, parsed.mbs, parsed.coefs)
+        ctx.decode()
+        ctx.synchronize()
+        dig = ctx.digests(np.arange(parsed.npics))
+        for p in (0, parsed.npics - 1):
+            got = ctx.download(p)
+            assert all(np.array_equal(got[k], exp[p][k]) for k in range(3)), (config, p)
+    assert [int(x) for x in dig] == [R.planes_digest(f) for f in exp]

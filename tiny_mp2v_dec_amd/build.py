@@ -57,7 +57,12 @@ def build(verbose=False):
     hdrs = _headers()
     jobs = []
     objs = []
+    # a library newer than every source and header is current even when its objects are absent
+    # (they are gpurun-ignored, so the GPU box gets the .so alone)
+    lib_current = not _stale(LIB, srcs + hdrs)
     for s in srcs:
+        if lib_current:
+            break
         o = os.path.join(OUT, os.path.basename(s) + ".o")
         objs.append(o)
         if _stale(o, [s] + hdrs):
@@ -67,7 +72,7 @@ def build(verbose=False):
             for o in ex.map(lambda j: _compile(*j), jobs):
                 if verbose:
                     print("built", os.path.relpath(o, REPO))
-    if _stale(LIB, objs):
+    if not lib_current and _stale(LIB, objs):
         cmd = [_hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", LIB] + objs + ["-lpthread"]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
