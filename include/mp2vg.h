@@ -118,8 +118,14 @@ typedef struct mp2vg_config {
     int32_t num_threads;         /* host parse threads (0 = auto)                            */
     int32_t reordering;          /* display reorder in the drop-in decoder                   */
     int32_t device;              /* HIP device ordinal                                       */
-    int32_t reserved;
+    int32_t reserved;            /* drop-in decoder flags (MP2VG_DECODER_*), else 0          */
 } mp2vg_config_t;
+
+/* mp2vg_config_t.reserved flag for mp2vg_decoder_create: frames are handed to the renderer in
+ * HBM (mp2vg_frame_t.planes are device pointers on cfg->device, valid during the callback), with
+ * no PCIe download: the opt-in device-pointer output path for callers that consume frames on the
+ * GPU.  Without it, planes are host memory (the reference's frame_c contract). */
+#define MP2VG_DECODER_DEVICE_FRAMES 1
 
 typedef struct mp2vg_ctx mp2vg_ctx_t;
 
@@ -212,7 +218,8 @@ void mp2vg_free(void* ptr);
 
 /* ---- drop-in decoder (reference mp2v_decoder_c) ---------------------------------------- */
 typedef struct mp2vg_frame {
-    uint8_t* planes[3];       /* host copy, valid only during the callback (frame_c rule)   */
+    uint8_t* planes[3];       /* host copy (device pointer with MP2VG_DECODER_DEVICE_FRAMES),
+                                 valid only during the callback (frame_c rule)               */
     int32_t  width[3], height[3], stride[3];
     int32_t  picture_coding_type;
     int32_t  decode_index;

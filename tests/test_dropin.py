@@ -106,3 +106,30 @@ def test_dropin_bad_stream_fails_cleanly_then_recovers():
     dec.decode(good)
     dec.close()
     assert got == exp
+
+
+def test_dropin_device_frames_match_host_frames():
+    """MP2VG_DECODER_DEVICE_FRAMES (the opt-in device-pointer output path, SURVEY §8b Output):
+    frames handed over in HBM, in the same display order and byte for byte the same as the host
+    frames of the reference's frame_c contract (which test_dropin_python_api pins to the
+    reference)."""
+    import hashlib
+    from tiny_mp2v_dec_amd.decoder import decoder_config_t, mp2v_decoder_c
+    e = next(m for m in MANIFEST if m["name"] == "ipb420_qcif")
+    es = read_stream(e)
+    out = {}
+    for dev in (False, True):
+        got = []
+
+        def render(frame, got=got, dev=dev):
+            assert frame.is_device == dev
+            if dev:
+                assert frame.device_ptr(0)
+            got.append((frame.decode_index, hashlib.md5(frame.yuv_bytes()).hexdigest()))
+
+        d = mp2v_decoder_c(decoder_config_t(e["width"], e["height"], e["chroma_format"], device_frames=dev), render)
+        d.decode(es, len(es))
+        d.close()
+        out[dev] = got
+    assert len(out[True]) == e["frames"]
+    assert out[True] == out[False]

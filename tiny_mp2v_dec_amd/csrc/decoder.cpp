@@ -46,7 +46,8 @@ constexpr int kMaxDl = 4;
 const int kDlStreams = getenv("MP2VG_DL_STREAMS") ? std::min(kMaxDl, std::max(1, atoi(getenv("MP2VG_DL_STREAMS")))) : 4;
 
 // Host frames live in pinned memory, in the device slot layout (= the reference frame_c layout),
-// so a decoded slot comes back with one contiguous DMA copy.  They are recycled after the render
+// so a decoded slot comes back with one contiguous DMA copy (with MP2VG_DECODER_DEVICE_FRAMES
+// they are HBM buffers and the copy is device to device, no PCIe).  They are recycled after the render
 // callback returns (a frame is valid only during the callback, reference threads.cpp:75-80).
 // The pool belongs to the decoder and is filled when it is created, as the reference allocates
 // its picture pool up front (decoder.cpp:381-406).
@@ -57,10 +58,13 @@ struct HostFrame {
 
 class FramePool {
   public:
-    explicit FramePool(size_t bytes) : bytes_(bytes) {}
+    FramePool(size_t bytes, bool device) : bytes_(bytes), device_(device) {}
     ~FramePool() {
         for (HostFrame* f : all_) {
-            hipHostFree(f->data);
+            if (device_)
+                hipFree(f->data);
+            else
+                hipHostFree(f->data);
             delete f;
         }
     }
@@ -91,7 +95,9 @@ class FramePool {
   private:
     HostFrame* alloc() {
         auto* f = new HostFrame();
-        if (hipHostMalloc((void**)&f->data, bytes_, hipHostMallocDefault) != hipSuccess) {
+        const hipError_t e = device_ ? hipMalloc((void**)&f->data, bytes_)
+                                     : hipHostMalloc((void**)&f->data, bytes_, hipHostMallocDefault);
+        if (e != hipSuccess) {
             delete f;
             return nullptr;
         }
@@ -100,6 +106,7 @@ class FramePool {
         return f;
     }
     size_t bytes_;
+    bool device_;
     std::mutex mu_;
     std::vector<HostFrame*> all_, free_;
 };
@@ -140,6 +147,7 @@ struct mp2vg_decoder {
     hipStream_t dl[kMaxDl] = {};
     int ndl = 1;
     hipEvent_t decoded = nullptr;      // end of the last chunk's decode (on the context stream)
+    bool device_frames = false;        // MP2VG_DECODER_DEVICE_FRAMES: frames handed over in HBM
 };
 
 extern "C" int mp2vg_decoder_destroy(mp2vg_decoder_t* d) {
@@ -160,6 +168,10 @@ extern "C" int mp2vg_decoder_create(const mp2vg_config_t* cfg, mp2vg_render_fn f
                                     mp2vg_decoder_t** out) {
     if (!cfg || !fn || !out) return MP2VG_E_INVALID;
     *out = nullptr;
+    if (cfg->reserved & ~MP2VG_DECODER_DEVICE_FRAMES) {
+        set_error("unknown decoder flags in mp2vg_config_t.reserved");
+        return MP2VG_E_INVALID;
+    }
     mp2vg_config_t c = *cfg;
     // chunk k decodes into its own slots while chunk k-1 is still being downloaded
     c.pictures_pool_size = std::max(cfg->pictures_pool_size, 2 * kChunk + 4);
@@ -173,7 +185,8 @@ extern "C" int mp2vg_decoder_create(const mp2vg_config_t* cfg, mp2vg_render_fn f
     d->ctx = ctx;
     d->g.init(c.width, c.height, c.chroma_format);
     d->nslots = c.pictures_pool_size;
-    d->pool.reset(new FramePool(d->g.slot_bytes));
+    d->device_frames = c.reserved & MP2VG_DECODER_DEVICE_FRAMES;
+    d->pool.reset(new FramePool(d->g.slot_bytes, d->device_frames));
     ctx_set_launch_timing(ctx, false);  // no per-launch events on the drop-in's chunk path
     d->ndl = kDlStreams;
     bool sok = true;
@@ -373,7 +386,9 @@ extern "C" int mp2vg_decoder_decode(mp2vg_decoder_t* d, const uint8_t* buf, uint
             hf->f.decode_index = p;
             void* src = nullptr;
             rc = mp2vg_slot_device_ptr(d->ctx, slot_of[p], &src);
-            if (rc == MP2VG_OK && hipMemcpyAsync(hf->data, src, d->g.slot_bytes, hipMemcpyDeviceToHost, d->dl[p % d->ndl]) != hipSuccess)
+            if (rc == MP2VG_OK && hipMemcpyAsync(hf->data, src, d->g.slot_bytes,
+                                                 d->device_frames ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost,
+                                                 d->dl[p % d->ndl]) != hipSuccess)
                 rc = MP2VG_E_HIP;
             if (rc != MP2VG_OK) {
                 pool.put(hf);

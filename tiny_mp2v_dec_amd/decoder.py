@@ -9,6 +9,10 @@ implemented over the C ABI (mp2vg_decoder_*): records are parsed on the host, re
 the HIP kernels on the GPU, and each frame is copied into a host frame with the reference's
 frame_c layout before the renderer runs.  A frame is valid only during the callback (reference
 frame pool recycling, threads.cpp:75-80); copy it to keep it.
+
+decoder_config_t(device_frames=True) opts into the device-pointer output path
+(MP2VG_DECODER_DEVICE_FRAMES): frames stay in HBM (no PCIe download), frame_c.device_ptr(i) gives
+the plane's device address and get_planes(i) copies the plane to the host on demand.
 """
 import ctypes
 from dataclasses import dataclass
@@ -28,20 +32,53 @@ class decoder_config_t:  # noqa: N801  (reference name)
     num_threads: int = 0
     reordering: bool = True
     device: int = 0
+    device_frames: bool = False
+
+
+MP2VG_DECODER_DEVICE_FRAMES = 1  # include/mp2vg.h
+_hip = None
+
+
+def _hip_lib():
+    global _hip
+    if _hip is None:
+        for name in ("libamdhip64.so", "/opt/rocm/lib/libamdhip64.so"):
+            try:
+                _hip = ctypes.CDLL(name)
+                break
+            except OSError:
+                continue
+        else:
+            raise RuntimeError("libamdhip64.so not found")
+        _hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    return _hip
 
 
 class frame_c:  # noqa: N801  (reference name)
     """View of one decoded frame (reference decoder.h:34-49)."""
 
-    def __init__(self, f):
+    def __init__(self, f, device=False):
         self._f = f
+        self.is_device = device
         self.picture_coding_type = f.picture_coding_type
         self.decode_index = f.decode_index
 
     def get_planes(self, i):
         """numpy view of plane i: height x stride bytes (only valid during the callback)."""
         n = self._f.stride[i] * self._f.height[i]
+        if self.is_device:  # device frame: copy the plane out of HBM (hipMemcpyDeviceToHost = 2)
+            out = np.empty((self._f.height[i], self._f.stride[i]), np.uint8)
+            src = ctypes.cast(self._f.planes[i], ctypes.c_void_p)
+            if _hip_lib().hipMemcpy(out.ctypes.data, src, n, 2) != 0:
+                raise RuntimeError("hipMemcpy of a device frame plane failed")
+            return out
         return np.ctypeslib.as_array(self._f.planes[i], shape=(n,)).reshape(self._f.height[i], self._f.stride[i])
+
+    def device_ptr(self, i):
+        """Device address of plane i (device_frames decoders only; valid during the callback)."""
+        if not self.is_device:
+            raise ValueError("host frame: use get_planes")
+        return ctypes.cast(self._f.planes[i], ctypes.c_void_p).value
 
     def get_strides(self, i):
         return self._f.stride[i]
@@ -62,11 +99,13 @@ class mp2v_decoder_c:  # noqa: N801  (reference name)
         self._renderer = renderer
         self._cfg = _lib.make_config(config.width, config.height, config.chroma_format, config.pictures_pool_size,
                                      config.num_threads, config.reordering, config.device)
+        self._device = bool(config.device_frames)
+        self._cfg.reserved = MP2VG_DECODER_DEVICE_FRAMES if self._device else 0
         self._error = None
 
         def _cb(user, fptr):
             try:
-                self._renderer(frame_c(fptr.contents))
+                self._renderer(frame_c(fptr.contents, self._device))
             except BaseException as e:  # surface renderer errors from decode()
                 if self._error is None:
                     self._error = e

@@ -35,6 +35,8 @@ def main():
     ap.add_argument("--threads", type=int, default=min(16, os.cpu_count() or 1))
     ap.add_argument("--ref", action="store_true", help="also time the real reference (oracle/_ref/ref_decode) "
                     "on the same stream and host")
+    ap.add_argument("--device-frames", action="store_true", help="drop-in with MP2VG_DECODER_DEVICE_FRAMES "
+                    "(frames handed over in HBM, no D2H)")
     a = ap.parse_args()
     w, h, cf, extra, desc = bench.CONFIGS[a.config]
     es = R.generate_es(width=w, height=h, chroma_format=cf, n_gops=a.gops, seed=1729, **extra)
@@ -66,7 +68,7 @@ def main():
     def render(frame):
         count[0] += 1
 
-    cfg = decoder_config_t(w, h, cf, pictures_pool_size=24, num_threads=a.threads)
+    cfg = decoder_config_t(w, h, cf, pictures_pool_size=24, num_threads=a.threads, device_frames=a.device_frames)
     dec = mp2v_decoder_c(cfg, render)
     t = time.perf_counter()
     dec.decode(es, len(es))
@@ -83,7 +85,7 @@ def main():
         "record_bytes_per_frame": int(rec_bytes / n),
         "device_fps": round(n / t_dev, 1),
         "download_GBps": round(frame_bytes * n / t_down / 1e9, 2), "download_fps": round(n / t_down, 1),
-        "dropin_fps": round(n / t_drop, 1),
+        "dropin_fps": round(n / t_drop, 1), "dropin_device_frames": a.device_frames,
         "pcie_inclusive_fps": round(n / (t_up + t_dev + t_down), 1),
     }
     if a.ref:
