@@ -44,8 +44,11 @@ private:
 class mp2v_decoder_c {
 public:
     mp2v_decoder_c() = default;
-    mp2v_decoder_c(const decoder_config_t& config, std::function<void(frame_c*)> renderer, int device = 0) {
-        decoder_init(config, renderer, device);
+    // flags: MP2VG_DECODER_DEVICE_FRAMES hands frames over in HBM (get_planes() then returns
+    // device pointers); 0 keeps the reference's host frame_c contract
+    mp2v_decoder_c(const decoder_config_t& config, std::function<void(frame_c*)> renderer, int device = 0,
+                   int flags = 0) {
+        decoder_init(config, renderer, device, flags);
     }
     ~mp2v_decoder_c() {
         if (m_dec) mp2vg_decoder_destroy(m_dec);
@@ -53,7 +56,8 @@ public:
     mp2v_decoder_c(const mp2v_decoder_c&) = delete;
     mp2v_decoder_c& operator=(const mp2v_decoder_c&) = delete;
 
-    bool decoder_init(const decoder_config_t& config, std::function<void(frame_c*)> renderer, int device = 0) {
+    bool decoder_init(const decoder_config_t& config, std::function<void(frame_c*)> renderer, int device = 0,
+                      int flags = 0) {
         m_render = renderer;
         mp2vg_config_t c{};
         c.width = config.width;
@@ -63,6 +67,7 @@ public:
         c.num_threads = config.num_threads;
         c.reordering = config.reordering ? 1 : 0;
         c.device = device;
+        c.reserved = flags;
         return mp2vg_decoder_create(&c, &mp2v_decoder_c::trampoline, this, &m_dec) == MP2VG_OK;
     }
     // reference decoder.h:99 — buffer is read as whole ES; returns after all frames rendered
