@@ -39,6 +39,10 @@ CONFIGS = {
 }
 
 
+# GOPs per GPU per step (c5: I-only, one picture per "GOP"; c4: 4K, 192 frames = 2.4 GB per step)
+DEFAULT_GOPS = {"c2": 64, "c3": 64, "c4": 16, "c5": 64}
+
+
 def algorithmic_bytes(parsed):
     """B_out + B_ref + B_rec for the batch.
     B_out = visible plane bytes per frame; B_ref = 384/512/768 B per predicted MB per direction;
@@ -58,6 +62,34 @@ def algorithmic_bytes(parsed):
     b_ref = dirs * mb_bytes
     b_rec = 32 * len(parsed.mbs) + 4 * len(parsed.coefs)
     return b_out + b_ref + b_rec, dict(out=b_out, ref=b_ref, rec=b_rec)
+
+
+def per_picture_bytes(parsed):
+    """algorithmic_bytes split by picture (decode order): frame bytes + its MBs' reference bytes +
+    its records and coefficient words.  Summed per kernel launch for the per-kernel roofline."""
+    cf = parsed.chroma_format
+    w, h = parsed.width, parsed.height
+    cw = w if cf == 3 else w // 2
+    ch = h if cf != 1 else h // 2
+    frame = w * h + 2 * cw * ch
+    mb_bytes = {1: 384, 2: 512, 3: 768}[cf]
+    n = int(parsed.pics[0]["mb_width"]) * int(parsed.pics[0]["mb_height"])
+    fl = parsed.mbs["flags"].astype(np.int64).reshape(parsed.npics, n)
+    inter = (fl & 1) == 0
+    dirs = inter * ((((fl & 2) != 0) | (inter & ((fl & 4) == 0))).astype(np.int64) + ((fl & 4) != 0))
+    ncoef = parsed.mbs["ncoef"].astype(np.int64).reshape(parsed.npics, n)
+    return frame + mb_bytes * dirs.sum(1) + 32 * n + 4 * ncoef.sum(1)
+
+
+def expected_digests(config, gops, seed):
+    """Per-slot (decode order) frame digests of this bench workload from the compiled reference
+    (tests/golden/bench_digests.npz, written by tests/golden/make_bench_digests.py), or None."""
+    path = os.path.join(REPO, "tests", "golden", "bench_digests.npz")
+    if not os.path.exists(path):
+        return None
+    with np.load(path) as d:
+        key = f"{config}_g{gops}_s{seed}"
+        return d[key].copy() if key in d else None
 
 
 def cpu_baseline(es, width, height, cf, frames):
@@ -116,20 +148,33 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--gops", type=int, default=64)
+    ap.add_argument("--gops", type=int, default=None, help="GOPs per GPU (default: DEFAULT_GOPS[config])")
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="torch.distributed backend for N>1 (gloo: CPU collectives; lets several ranks "
+                         "share one GPU to rehearse the multi-GPU path)")
+    ap.add_argument("--gather-gops", type=int, default=8,
+                    help="GOPs per rank in the rank-0 frame gather measured after the timed region")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the drop-in end-to-end measurement")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    coll_dev = "cpu"
+    import torch
+    ndev = max(1, torch.cuda.device_count())  # does not initialise the GPU
+    device = local_rank % ndev
     if world > 1:
-        import torch
         import torch.distributed as tdist
-        torch.cuda.set_device(local_rank)
-        tdist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if args.backend == "nccl":
+            torch.cuda.set_device(device)
+            tdist.init_process_group("nccl", device_id=torch.device("cuda", device))
+            coll_dev = f"cuda:{device}"
+        else:
+            tdist.init_process_group("gloo")
         dist = tdist
 
     if rank == 0:
@@ -137,14 +182,17 @@ def main():
     if dist is not None:
         dist.barrier()
 
+    from tiny_mp2v_dec_amd import gather as G
+
     width, height, cf, gparams, desc = CONFIGS[args.config]
     # c5 is I-only: one picture per "GOP", so --gops is its frame count (~60 frames; at
     # 768 frames its elementary stream would pass the 2 GB `int len` of the reference decode() API)
-    gops = args.gops
-    es = R.generate_es(width=width, height=height, chroma_format=cf, n_gops=gops, seed=1729 + rank, **gparams)
+    gops = args.gops or DEFAULT_GOPS[args.config]
+    seed = 1729 + rank
+    es = R.generate_es(width=width, height=height, chroma_format=cf, n_gops=gops, seed=seed, **gparams)
     parsed = R.Parsed(es, width, height, cf, threads=min(8, os.cpu_count() or 1))
     alg_bytes, parts = algorithmic_bytes(parsed)
-    ctx = R.DeviceContext(width, height, cf, slots=parsed.npics, device=local_rank)
+    ctx = R.DeviceContext(width, height, cf, slots=parsed.npics, device=device)
     ctx.upload(parsed.pics, parsed.mbs, parsed.coefs)
 
     for _ in range(args.warmup):
@@ -171,21 +219,100 @@ def main():
         b, l = ctx.batch_times(back)
         batch_ms.append(b)
         kernel_ms.append(l)
-    if dist is not None:
-        import torch
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = G.max_over_ranks(elapsed, dist, coll_dev)
 
-    # frame gather (digests) to rank 0 over RCCL, outside the timed region
+    # ---- parity of the timed batch: device digest of every frame vs the compiled reference's ----
     dig = ctx.digests(np.arange(parsed.npics))
-    gathered = [dig]
+    exp = expected_digests(args.config, gops, seed)
+    my_status = 2 if exp is None else (1 if np.array_equal(dig, exp) else 0)  # 2 unchecked, 1 ok, 0 bad
+    gathered = G.gather_u64(dig, dist, coll_dev)
+    statuses = [int(x[0]) for x in G.gather_u64(np.array([my_status], np.uint64), dist, coll_dev)]
+    if any(s == 0 for s in statuses):
+        parity = {"status": "MISMATCH", "ranks_mismatching": [r for r, s in enumerate(statuses) if s == 0]}
+    elif all(s == 1 for s in statuses):
+        parity = {"status": "bit-exact", "frames_checked": int(sum(len(g) for g in gathered)),
+                  "against": "tests/golden/bench_digests.npz: per-frame digests of the compiled reference "
+                             "decoder (1 thread) on each rank's stream"}
+    else:
+        parity = {"status": "unchecked", "why": "no reference digests for this workload/seed in "
+                                                "tests/golden/bench_digests.npz"}
+
+    # ---- per-kernel roofline: the same batch on a one-stream context, so launches never overlap ----
+    of_pic, modes = R.plan_batch(width, height, cf, parsed.npics, parsed.pics, parsed.mbs, parsed.coefs,
+                                 one_stream=True)
+    pic_bytes = per_picture_bytes(parsed)
+    launch_bytes = np.bincount(of_pic, weights=pic_bytes, minlength=len(modes))
+    ctx1 = R.DeviceContext(width, height, cf, slots=parsed.npics, device=device, one_stream=True)
+    ctx1.upload(parsed.pics, parsed.mbs, parsed.coefs)
+    k1 = 5
+    for _ in range(k1 + 1):
+        ctx1.decode()
+    ctx1.synchronize()
+    l1 = np.array([ctx1.batch_times(back)[1] for back in range(k1)])  # (k1, launches)
+    span1 = float(np.mean([ctx1.batch_times(back)[0] for back in range(k1)]))
+    if exp is not None and not np.array_equal(ctx1.digests(np.arange(parsed.npics)), exp):
+        parity = {"status": "MISMATCH", "ranks_mismatching": [rank], "context": "one-stream"}
+    ctx1.close()
+    per_kernel = {}
+    for m in sorted(set(modes.tolist())):
+        sel = modes == m
+        ms = float(l1[:, sel].mean(axis=0).sum())
+        nbytes = float(launch_bytes[sel].sum())
+        name = f"recon_kernel<{cf}, {m}, 0>"
+        per_kernel[name] = {"mode": ["I", "P", "B", "P+B"][m], "launches_per_step": int(sel.sum()),
+                            "avg_launch_ms": round(ms / int(sel.sum()), 4),
+                            "algorithmic_bytes_per_launch": int(nbytes / int(sel.sum())),
+                            "achieved_GBps": round(nbytes / (ms / 1e3) / 1e9, 1),
+                            "frac": round(nbytes / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                            "share_of_step": round(ms / float(l1.sum(axis=1).mean()), 3)}
+    dominant = max(per_kernel, key=lambda k: per_kernel[k]["share_of_step"])
+
+    # ---- rank-0 frame gather (grouped send/recv per round of GOPs, display order), timed apart ----
+    gather_res = None
     if dist is not None:
-        import torch
-        d = torch.from_numpy(dig.view(np.int64)).cuda()
-        outs = [torch.empty_like(d) for _ in range(world)]
-        dist.all_gather(outs, d)
-        gathered = [o.cpu().numpy().view(np.uint64) for o in outs]
+        ng = min(args.gather_gops, int(parsed.gop.max()) + 1)
+        fb = ctx.frame_bytes()
+        on_dev = coll_dev != "cpu"
+        gop_sizes, gop_frames = [], {}
+        for g in range(ng * world):  # virtual stream: GOP g = GOP g // world of rank g % world
+            local = [int(d) for d in parsed.display if parsed.gop[d] == g // world]
+            gop_sizes.append(len(local))
+            if g % world == rank:
+                fr = []
+                for d in local:
+                    t = torch.empty(fb, dtype=torch.uint8, device=coll_dev)
+                    ctx.copy_packed(d, t.data_ptr(), on_dev)
+                    fr.append(t)
+                gop_frames[g] = fr
+        if on_dev:
+            torch.cuda.synchronize()
+        barrier()
+        tg = time.perf_counter()
+        got = G.gather_gops(dist, gop_frames, gop_sizes, fb, device=coll_dev)
+        if on_dev:
+            torch.cuda.synchronize()
+        tg = G.max_over_ranks(time.perf_counter() - tg, dist, coll_dev)
+        if rank == 0:
+            # spot-check: the first and last gathered frame of every rank == that rank's device digest
+            # of the same picture (every rank's stream has the same GOP structure, so rank 0's own
+            # display order and GOP index map a gathered position to the sender's decode index)
+            pw, ph = ctx.pw, ctx.ph
+            starts = np.concatenate([[0], np.cumsum(gop_sizes)])
+            ok = True
+            for r in range(min(world, ng * world)):
+                for g in (r, r + world * (ng - 1)):
+                    local = [int(d) for d in parsed.display if parsed.gop[d] == g // world]
+                    for k in (0, len(local) - 1):
+                        buf = got[int(starts[g]) + k].cpu().numpy()
+                        planes, o = [], 0
+                        for i in range(3):
+                            planes.append(buf[o:o + pw[i] * ph[i]].reshape(ph[i], pw[i]))
+                            o += pw[i] * ph[i]
+                        ok &= R.planes_digest(planes) == int(gathered[r][local[k]])
+            gather_res = {"frames": len(got), "bytes": int(len(got) * fb), "ms": round(tg * 1e3, 3),
+                          "GBps_into_rank0": round(len(got) * fb / tg / 1e9, 2), "verified": bool(ok),
+                          "sample": f"first {ng} GOPs of every rank, frame by frame in display order"}
+        del gop_frames, got
 
     traffic = profiled_traffic(args.config, gops)
     frames_total = parsed.npics * world * args.steps
@@ -211,7 +338,8 @@ def main():
         "config": {"workload": f"{desc}, pre-parsed MB records resident in HBM, {gops} GOPs per GPU",
                    "width": width, "height": height, "chroma_format": {1: "4:2:0", 2: "4:2:2", 3: "4:4:4"}[cf],
                    "frames_per_gpu_per_step": parsed.npics, "global_batch_frames": parsed.npics * world,
-                   "parallelism": f"gop-shard x{world}"},
+                   "parallelism": f"gop-shard x{world}", "backend": args.backend if world > 1 else None},
+        "parity": parity,
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic["traffic_bytes_per_step"] if traffic else None,
                      "traffic_unit": "bytes/step (HBM, PMC)", "traffic_source": traffic["source"] if traffic else None,
@@ -219,16 +347,56 @@ def main():
                      "avg_launch_ms": round(float(np.mean(per_launch)), 4),
                      "algorithmic_bytes_per_step": int(alg_bytes), "bytes_breakdown": parts,
                      "kernel_ms_per_step": round(kernel_step_ms, 4),
-                     "sum_launch_ms_per_step": round(float(np.mean([sum(s) for s in kernel_ms])), 4)},
+                     "sum_launch_ms_per_step": round(float(np.mean([sum(s) for s in kernel_ms])), 4),
+                     "dominant_kernel": dominant, "one_stream_span_ms": round(span1, 4),
+                     "per_kernel": per_kernel},
         "frame_digest_of_digests": int(np.bitwise_xor.reduce(np.concatenate(gathered))),
     }
+    if gather_res is not None:
+        result["frame_gather"] = gather_res
+    ctx.close()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(es, width, height, cf, parsed.npics)
+    if rank == 0 and world == 1 and not args.no_e2e:
+        result["e2e_dropin"] = e2e_dropin(es, width, height, cf, parsed.npics, device,
+                                          result.get("cpu_baseline"))
     if rank == 0:
         print(json.dumps(result), flush=True)
-    ctx.close()
     if dist is not None:
         dist.destroy_process_group()
+    if parity["status"] == "MISMATCH":
+        sys.exit(3)
+
+
+def e2e_dropin(es, width, height, cf, frames, device, cpu):
+    """The drop-in API end to end on the same stream: mp2v_decoder_c(config, renderer).decode(buf)
+    with host frame_c frames (parse, upload, decode, D2H, display-order render callbacks), i.e.
+    what a caller of the reference API sees (reference tiny_mp2v_dec.cpp:50-55 times decode()
+    the same way).  PCIe-inclusive: never the bench `value`."""
+    from tiny_mp2v_dec_amd.decoder import decoder_config_t, mp2v_decoder_c
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 2)
+    threads = max(2, min(share, os.cpu_count() or share, 16))
+    count = [0]
+
+    def render(frame):
+        count[0] += 1
+
+    dec = mp2v_decoder_c(decoder_config_t(width, height, cf, pictures_pool_size=24, num_threads=threads,
+                                          device=device), render)
+    try:
+        t = time.perf_counter()
+        dec.decode(es, len(es))
+        dt = time.perf_counter() - t
+    finally:
+        dec.close()
+    if count[0] != frames:
+        raise RuntimeError(f"drop-in rendered {count[0]} of {frames} frames")
+    out = {"value": round(frames / dt, 1), "unit": "frames/s", "host_threads": threads, "frames": frames,
+           "scope": "drop-in mp2v_decoder_c::decode() on the bench stream: host parse + record upload + "
+                    "GPU reconstruct + D2H into host frame_c + render callbacks"}
+    if cpu:
+        out["vs_cpu_baseline"] = round(out["value"] / cpu["value"], 3)
+    return out
 
 
 if __name__ == "__main__":

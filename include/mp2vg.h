@@ -118,7 +118,7 @@ typedef struct mp2vg_config {
     int32_t num_threads;         /* host parse threads (0 = auto)                            */
     int32_t reordering;          /* display reorder in the drop-in decoder                   */
     int32_t device;              /* HIP device ordinal                                       */
-    int32_t reserved;            /* drop-in decoder flags (MP2VG_DECODER_*), else 0          */
+    int32_t reserved;            /* flags: MP2VG_DECODER_* (drop-in decoder), MP2VG_CTX_*     */
 } mp2vg_config_t;
 
 /* mp2vg_config_t.reserved flag for mp2vg_decoder_create: frames are handed to the renderer in
@@ -126,6 +126,10 @@ typedef struct mp2vg_config {
  * no PCIe download: the opt-in device-pointer output path for callers that consume frames on the
  * GPU.  Without it, planes are host memory (the reference's frame_c contract). */
 #define MP2VG_DECODER_DEVICE_FRAMES 1
+/* mp2vg_config_t.reserved flag for mp2vg_create: run every picture set of a batch on one stream
+ * (default: closed groups of pictures dealt to 2 streams, or MP2VG_STREAMS), so per-launch
+ * device times never overlap -- per-kernel roofline measurements and their rocprof traces */
+#define MP2VG_CTX_ONE_STREAM 2
 
 typedef struct mp2vg_ctx mp2vg_ctx_t;
 
@@ -146,6 +150,16 @@ int  mp2vg_reserve_slots(mp2vg_ctx_t* ctx, int32_t nslots);
 int  mp2vg_batch_upload(mp2vg_ctx_t* ctx, const mp2vg_picture_t* pics, int32_t npics,
                         const mp2vg_mb_t* mbs, uint64_t nmbs, const uint32_t* coefs,
                         uint64_t ncoefs);
+/* Host-only check of a record batch against a geometry and a pool of nslots slots: exactly the
+ * validation and planning mp2vg_batch_upload runs before any copy (no device needed).  Returns
+ * MP2VG_OK, or MP2VG_E_INVALID with the reason in mp2vg_last_error().  Optional outputs (NULL to
+ * skip): *nlaunches = kernel launches per mp2vg_batch_decode; launch_of_pic[npics] = the launch
+ * (index into mp2vg_batch_times' launch list) that reconstructs each picture; launch_mode[i <
+ * max_launches] = that launch's kernel (0 I, 1 P, 2 B, 3 mixed P/B picture types). */
+int  mp2vg_batch_validate(const mp2vg_config_t* cfg, int32_t nslots, const mp2vg_picture_t* pics,
+                          int32_t npics, const mp2vg_mb_t* mbs, uint64_t nmbs,
+                          const uint32_t* coefs, uint64_t ncoefs, int32_t* nlaunches,
+                          int32_t* launch_of_pic, int32_t* launch_mode, int32_t max_launches);
 /* Enqueue the reconstruct of every picture of the resident batch: pictures are grouped by
  * reference-dependency depth and each depth level is one kernel launch (one workgroup per
  * slice = MB row).  Asynchronous; per-launch device times are recorded with HIP events. */
@@ -164,6 +178,10 @@ int  mp2vg_batch_times(mp2vg_ctx_t* ctx, int32_t back, float* batch_ms, float* l
  * dst_stride is 0); synchronous */
 int  mp2vg_download_slot(mp2vg_ctx_t* ctx, int32_t slot, uint8_t* dst_planes[3],
                          const int32_t dst_stride[3]);
+/* copy one frame slot's visible planes Y, U, V tightly packed (the reference sample's write_yuv
+ * layout, tiny_mp2v_dec.cpp:11-17) to dst: HBM of the context's device when dst_on_device
+ * (e.g. an RCCL send buffer for the rank-0 frame gather), else host memory; synchronous */
+int  mp2vg_copy_slot_packed(mp2vg_ctx_t* ctx, int32_t slot, void* dst, int32_t dst_on_device);
 /* raw device pointer of a slot (for in-HBM consumers such as a digest kernel or RCCL) */
 int  mp2vg_slot_device_ptr(mp2vg_ctx_t* ctx, int32_t slot, void** dptr);
 /* 64-bit order-independent digest of each listed slot's visible planes, computed on device:
@@ -189,6 +207,19 @@ int  mp2vg_parsed_display_order(const mp2vg_parsed_t* p, int32_t* order, int32_t
 /* GOP index (0-based, by group_start_code) of each picture, for GOP sharding */
 int  mp2vg_parsed_gop_index(const mp2vg_parsed_t* p, int32_t* gop, int32_t n);
 void mp2vg_parsed_free(mp2vg_parsed_t* p);
+
+/* Conformance hook: decode one Annex B code (MSB-first 64-bit window: the code, then whatever
+ * follows) with the emitter's own decoders.  Tables follow the reference's VLC decoders
+ * (mp2v_vlc_dec.hpp:36-267) except where the emitter reads more: MOTION consumes the sign bit
+ * and returns the signed motion_code; COEF_B14/B15 consume the sign bit (or the escape's run
+ * and level) and return run in *value and the signed level in *aux (EOB: *value = -1); MBA
+ * returns -33 for macroblock_escape.  Returns MP2VG_E_BITSTREAM for an invalid code. */
+enum {
+    MP2VG_VLC_MBA = 0, MP2VG_VLC_MBTYPE_I = 1, MP2VG_VLC_MBTYPE_P = 2, MP2VG_VLC_MBTYPE_B = 3,
+    MP2VG_VLC_CBP = 4, MP2VG_VLC_MOTION = 5, MP2VG_VLC_DC_LUMA = 6, MP2VG_VLC_DC_CHROMA = 7,
+    MP2VG_VLC_COEF_B14 = 8, MP2VG_VLC_COEF_B15 = 9
+};
+int  mp2vg_vlc_decode(int32_t table, uint64_t bits, int32_t* value, int32_t* aux, int32_t* consumed);
 
 /* ---- synthetic stream writer (the accepted subset only) --------------------- */
 typedef struct mp2vg_gen_params {

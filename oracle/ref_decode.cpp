@@ -9,6 +9,7 @@
 //
 // usage: ref_decode <in.m2v> <width> <height> <chroma_format 1|2|3> <threads> <out.yuv|-> [repeat]
 //   out "-" : decode without writing (timing mode).
+//   out "*.dig" : write one uint64 frame digest per frame in display order instead of the YUV.
 // prints one JSON line: {"frames": F, "ms": best-of-repeat decode() wall time, "threads": T}
 #include <chrono>
 #include <cstdio>
@@ -23,6 +24,29 @@ static void write_yuv(FILE* fp, frame_c* frame) {
         for (int y = 0; y < frame->get_height(i); y++, plane += frame->get_strides(i))
             fwrite(plane, 1, frame->get_width(i), fp);
     }
+}
+
+// Per-frame 64-bit digest of the visible planes, the host twin of the device digest
+// (tiny_mp2v_dec_amd.records.planes_digest): sum over visible little-endian dwords d at
+// (row_id, byte x), rows numbered across Y, U, V, of mix64((row_id << 32) | x) ^ d, mod 2^64.
+static uint64_t mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+static uint64_t frame_digest(frame_c* frame) {
+    uint64_t acc = 0, row_id = 0;
+    for (int i = 0; i < 3; i++) {
+        const uint8_t* plane = frame->get_planes(i);
+        for (int y = 0; y < frame->get_height(i); y++, plane += frame->get_strides(i), row_id++)
+            for (int x = 0; x + 4 <= frame->get_width(i); x += 4) {
+                uint32_t d;
+                memcpy(&d, plane + x, 4);
+                acc += mix64((row_id << 32) | (uint64_t)x) ^ (uint64_t)d;
+            }
+    }
+    return acc;
 }
 
 int main(int argc, char** argv) {
@@ -53,6 +77,8 @@ int main(int argc, char** argv) {
     int repeat = argc > 7 ? atoi(argv[7]) : 1;
 
     FILE* out = nullptr;
+    const size_t olen = strlen(out_path);
+    const bool digest = olen > 4 && !strcmp(out_path + olen - 4, ".dig");
     if (strcmp(out_path, "-") != 0) {
         out = fopen(out_path, "wb");
         if (!out) { perror(out_path); return 1; }
@@ -64,9 +90,14 @@ int main(int argc, char** argv) {
         FILE* fp = (r == 0) ? out : nullptr;
         auto t0 = std::chrono::steady_clock::now();
         {
-            mp2v_decoder_c dec(cfg, [fp, &nframes](frame_c* f) {
+            mp2v_decoder_c dec(cfg, [fp, digest, &nframes](frame_c* f) {
                 nframes++;
-                if (fp) write_yuv(fp, f);
+                if (fp && digest) {
+                    const uint64_t d = frame_digest(f);
+                    fwrite(&d, sizeof d, 1, fp);
+                } else if (fp) {
+                    write_yuv(fp, f);
+                }
             });
             dec.decode(buf.data(), (int)padded);
         }  // destructor joins the render + worker threads: all frames delivered

@@ -104,3 +104,71 @@ def test_shard_rejects_open_gop_cross_reference():
     p.mbs["flags"][first] = 2
     with pytest.raises(ValueError):
         shard_batch(p, 1, 2)
+
+
+def _gather_worker(rank, world, port, es, q):
+    """GOP-sharded decode (oracle as the CPU stand-in for the kernel) + the collectives bench.py
+    runs: max-over-ranks time, the digest all_gather and the rank-0 frame gather in display order."""
+    import sys
+    sys.path[:0] = [REPO, os.path.join(REPO, "tests")]
+    import torch
+    from helpers import oracle_frames
+    from tiny_mp2v_dec_amd import gather as G
+    from tiny_mp2v_dec_amd.records import Parsed, frame_yuv_bytes
+    from tiny_mp2v_dec_amd.shard import shard_batch
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    parsed = Parsed(es, 176, 144, 1)
+    pics, mbs, coefs, ids = shard_batch(parsed, rank, world)
+
+    class P:
+        pass
+
+    sp = P()
+    sp.width, sp.height, sp.chroma_format = 176, 144, 1
+    sp.pics, sp.mbs, sp.coefs, sp.npics = pics, mbs, coefs, len(pics)
+    frames = dict(zip((int(i) for i in ids), oracle_frames(sp)))  # full-stream decode index -> planes
+    ngops = int(parsed.gop.max()) + 1
+    sizes = [int(np.sum(parsed.gop == g)) for g in range(ngops)]
+    mine = {}
+    for g in range(ngops):
+        if g % world == rank:
+            disp = [int(d) for d in parsed.display if parsed.gop[d] == g]
+            mine[g] = [torch.from_numpy(np.frombuffer(frame_yuv_bytes(frames[d]), np.uint8).copy()) for d in disp]
+    fb = 176 * 144 * 3 // 2
+    got = G.gather_gops(dist, mine, sizes, fb)
+    mx = G.max_over_ranks(float(rank + 1), dist)
+    u = G.gather_u64(np.arange(rank + 2, dtype=np.uint64) + np.uint64(1 << 63), dist)
+    if rank == 0:
+        q.put(([bytes(t.numpy()) for t in got], mx, [x.tolist() for x in u]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_rank0_frame_gather_display_order(world):
+    """gather.gather_gops over gloo: rank 0 ends with every frame of the stream in display order,
+    byte-identical to a single-process decode written in the reference's write_yuv layout."""
+    import sys
+    sys.path[:0] = [REPO, os.path.join(REPO, "tests")]
+    from helpers import oracle_frames
+    from tiny_mp2v_dec_amd.records import Parsed, frame_yuv_bytes, generate_es
+
+    es = generate_es(width=176, height=144, chroma_format=1, n_gops=4, gop_n=6, gop_m=3, seed=78)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gather_worker, args=(r, world, port, es, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got, mx, u = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    full = Parsed(es, 176, 144, 1)
+    fr = oracle_frames(full)
+    assert got == [frame_yuv_bytes(fr[d]) for d in full.display]
+    assert mx == float(world)
+    assert u == [[(1 << 63) + k for k in range(r + 2)] for r in range(world)]

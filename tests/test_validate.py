@@ -1,0 +1,62 @@
+"""CPU: the record-batch validation mp2vg_batch_upload runs before any copy
+(mp2vg_batch_validate, no device): batches the parser emits pass, and batches no kernel may see
+are refused with MP2VG_E_INVALID."""
+import numpy as np
+import pytest
+
+from tiny_mp2v_dec_amd import _lib
+from tiny_mp2v_dec_amd import records as R
+
+
+def _parsed(cf=1, fpfd=1, seed=5, w=176, h=144):
+    es = R.generate_es(width=w, height=h, chroma_format=cf, n_gops=1, gop_n=12, gop_m=3,
+                       frame_pred_frame_dct=fpfd, seed=seed)
+    return R.Parsed(es, w, h, cf)
+
+
+@pytest.mark.parametrize("cf", [1, 2, 3])
+def test_parsed_batches_validate(cf):
+    p = _parsed(cf, fpfd=0)
+    n = R.validate_batch(p.width, p.height, cf, p.npics, p.pics, p.mbs, p.coefs)
+    assert 1 <= n <= 2 * 6  # one launch per dependency level and picture set
+
+
+def test_444_field_dct_record_rejected():
+    """4:4:4 dct_type=1: the reference puts blocks 10/11 at (dct_type ? 1 : 8) * stride + 8 with the
+    doubled luma stride (mb_decoder.cpp:193-194); the kernel's spec placement would diverge
+    silently, so the upload refuses such records."""
+    p = _parsed(3, fpfd=0)
+    mbs = p.mbs.copy()
+    coded = np.nonzero(mbs["cbp"] != 0)[0]
+    assert len(coded)
+    mbs["flags"][coded[0]] |= _lib.MB_DCT_FIELD
+    with pytest.raises(_lib.Mp2vgError, match="4:4:4 field-DCT"):
+        R.validate_batch(p.width, p.height, 3, p.npics, p.pics, mbs, p.coefs)
+    # 4:2:0 / 4:2:2 field DCT is fine
+    q = _parsed(2, fpfd=0)
+    m2 = q.mbs.copy()
+    m2["flags"][np.nonzero(m2["cbp"] != 0)[0][0]] |= _lib.MB_DCT_FIELD
+    R.validate_batch(q.width, q.height, 2, q.npics, q.pics, m2, q.coefs)
+
+
+def test_malformed_batches_rejected():
+    p = _parsed(1)
+    args = (p.width, p.height, 1, p.npics)
+
+    def bad(pics=p.pics, mbs=p.mbs, coefs=p.coefs, nslots=p.npics, match=None):
+        with pytest.raises(_lib.Mp2vgError, match=match):
+            R.validate_batch(p.width, p.height, 1, nslots, pics, mbs, coefs)
+
+    pics = p.pics.copy(); pics[1]["dst_slot"] = p.npics
+    bad(pics=pics, match="slot out of range")
+    mbs = p.mbs.copy(); mbs[3]["x"] += 1
+    bad(mbs=mbs, match="raster order")
+    mbs = p.mbs.copy(); mbs[0]["cbp"] = 1 << 6
+    bad(mbs=mbs, match="cbp")
+    coefs = p.coefs.copy(); coefs[0] ^= 1 << 28
+    bad(coefs=coefs, match="column mod 8")
+    mbs = p.mbs.copy(); k = int(np.nonzero(mbs["ncoef"])[0][-1]); mbs[k]["coef_off"] = len(p.coefs)
+    bad(mbs=mbs, match="outside the batch")
+    pics = p.pics.copy(); pics[1]["fwd_slot"] = -1; pics[1]["bwd_slot"] = -1
+    bad(pics=pics, match="missing reference")
+    R.validate_batch(*args, p.pics, p.mbs, p.coefs)

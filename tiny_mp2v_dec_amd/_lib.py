@@ -72,10 +72,10 @@ RENDER_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.POINTER(Frame))
 # every symbol declared in include/mp2vg.h
 EXPORTS = [
     "mp2vg_abi_version", "mp2vg_status_string", "mp2vg_last_error", "mp2vg_create", "mp2vg_destroy",
-    "mp2vg_frame_geometry", "mp2vg_reserve_slots", "mp2vg_batch_upload", "mp2vg_batch_decode",
-    "mp2vg_synchronize", "mp2vg_last_launch_times", "mp2vg_last_batch_time", "mp2vg_batch_times", "mp2vg_download_slot", "mp2vg_slot_device_ptr",
+    "mp2vg_frame_geometry", "mp2vg_reserve_slots", "mp2vg_batch_upload", "mp2vg_batch_validate", "mp2vg_batch_decode",
+    "mp2vg_synchronize", "mp2vg_last_launch_times", "mp2vg_last_batch_time", "mp2vg_batch_times", "mp2vg_download_slot", "mp2vg_copy_slot_packed", "mp2vg_slot_device_ptr",
     "mp2vg_slot_digests", "mp2vg_parse_es", "mp2vg_parsed_counts", "mp2vg_parsed_pictures", "mp2vg_parsed_mbs",
-    "mp2vg_parsed_coefs", "mp2vg_parsed_display_order", "mp2vg_parsed_gop_index", "mp2vg_parsed_free",
+    "mp2vg_parsed_coefs", "mp2vg_parsed_display_order", "mp2vg_parsed_gop_index", "mp2vg_parsed_free", "mp2vg_vlc_decode",
     "mp2vg_gen_default_params", "mp2vg_generate_es", "mp2vg_free", "mp2vg_decoder_create",
     "mp2vg_decoder_decode", "mp2vg_decoder_destroy",
 ]
@@ -101,12 +101,15 @@ def lib():
         "mp2vg_frame_geometry": ([P(Config), P(I32), P(I32), P(I32), P(U64)], ctypes.c_int),
         "mp2vg_reserve_slots": ([VP, I32], ctypes.c_int),
         "mp2vg_batch_upload": ([VP, VP, I32, VP, U64, VP, U64], ctypes.c_int),
+        "mp2vg_batch_validate": ([P(Config), I32, VP, I32, VP, U64, VP, U64, P(I32), P(I32), P(I32), I32],
+                                 ctypes.c_int),
         "mp2vg_batch_decode": ([VP], ctypes.c_int),
         "mp2vg_synchronize": ([VP], ctypes.c_int),
         "mp2vg_last_launch_times": ([VP, P(ctypes.c_float), I32, P(I32)], ctypes.c_int),
         "mp2vg_last_batch_time": ([VP, P(ctypes.c_float)], ctypes.c_int),
         "mp2vg_batch_times": ([VP, I32, P(ctypes.c_float), P(ctypes.c_float), I32, P(I32)], ctypes.c_int),
         "mp2vg_download_slot": ([VP, I32, P(ctypes.c_void_p), P(I32)], ctypes.c_int),
+        "mp2vg_copy_slot_packed": ([VP, I32, VP, I32], ctypes.c_int),
         "mp2vg_slot_device_ptr": ([VP, I32, P(VP)], ctypes.c_int),
         "mp2vg_slot_digests": ([VP, P(I32), I32, P(ctypes.c_uint64)], ctypes.c_int),
         "mp2vg_parse_es": ([VP, U64, P(Config), P(VP)], ctypes.c_int),
@@ -117,6 +120,7 @@ def lib():
         "mp2vg_parsed_display_order": ([VP, P(I32), I32], ctypes.c_int),
         "mp2vg_parsed_gop_index": ([VP, P(I32), I32], ctypes.c_int),
         "mp2vg_parsed_free": ([VP], None),
+        "mp2vg_vlc_decode": ([I32, U64, P(I32), P(I32), P(I32)], ctypes.c_int),
         "mp2vg_gen_default_params": ([P(GenParams)], None),
         "mp2vg_generate_es": ([P(GenParams), P(VP), P(U64)], ctypes.c_int),
         "mp2vg_free": ([VP], None),
@@ -139,8 +143,11 @@ def check(status, what):
     return status
 
 
-def make_config(width, height, chroma_format, pool=10, threads=0, reordering=True, device=0):
-    return Config(width, height, chroma_format, pool, threads, 1 if reordering else 0, device, 0)
+MP2VG_DECODER_DEVICE_FRAMES, MP2VG_CTX_ONE_STREAM = 1, 2  # mp2vg_config_t.reserved flags
+
+
+def make_config(width, height, chroma_format, pool=10, threads=0, reordering=True, device=0, flags=0):
+    return Config(width, height, chroma_format, pool, threads, 1 if reordering else 0, device, flags)
 
 
 def geometry(width, height, chroma_format):

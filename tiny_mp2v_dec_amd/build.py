@@ -1,10 +1,14 @@
 """Build the native library in-tree: tiny_mp2v_dec_amd/_build/libmp2vg.so (hipcc, gfx950 only).
 
-The .so is git-ignored but travels to the GPU box with the gpurun snapshot.  Incremental: an
-object is rebuilt when its source or any csrc/ header / include/ header is newer.
+The .so is git-ignored but travels to the GPU box with the gpurun snapshot.  Provenance is by
+content, not mtime: libmp2vg.so.stamp holds a SHA-256 over every source and header, the target
+arch and every compile / link command.  The library is current exactly when its stamp matches
+(so the GPU box, which gets the .so without objects, rebuilds nothing, and a change of
+MP2VG_OFFLOAD_ARCH or flags always rebuilds); each object carries the same kind of stamp.
 """
 import concurrent.futures
 import glob
+import hashlib
 import os
 import shutil
 import subprocess
@@ -30,24 +34,45 @@ def _headers():
     return glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(REPO, "include", "*.h"))
 
 
-def _stale(target, deps):
-    if not os.path.exists(target):
-        return True
-    t = os.path.getmtime(target)
-    return any(os.path.getmtime(d) > t for d in deps)
+def _digest(files, cmds):
+    h = hashlib.sha256()
+    for f in sorted(files):
+        h.update(os.path.relpath(f, REPO).encode() + b"\0")
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    for c in cmds:  # tool by name, in-tree paths relative to the repo (the GPU box's copy lives elsewhere)
+        h.update("\0".join(os.path.basename(x) if x == c[0] else x.replace(REPO, "<repo>") for x in c).encode()
+                 + b"\n")
+    return h.hexdigest()
 
 
-def _compile(src, obj):
-    hipcc = _hipcc()
+def _current(target, stamp):
+    try:
+        with open(target + ".stamp") as fh:
+            return os.path.exists(target) and fh.read().strip() == stamp
+    except OSError:
+        return False
+
+
+def _write_stamp(target, stamp):
+    with open(target + ".stamp", "w") as fh:
+        fh.write(stamp + "\n")
+
+
+def _compile_cmd(src, obj):
     common = ["-O3", "-fPIC", "-std=c++17", "-Wall", "-I", CSRC, "-I", os.path.join(REPO, "include")]
     if src.endswith(".hip"):
-        cmd = [hipcc, "-x", "hip", f"--offload-arch={ARCH}", "-munsafe-fp-atomics"] + common + ["-c", src, "-o", obj]
-    else:
-        # host translation units (HIP runtime API only): compiled as host C++ by hipcc
-        cmd = [hipcc, "-D__HIP_PLATFORM_AMD__"] + common + ["-c", src, "-o", obj]
+        return [_hipcc(), "-x", "hip", f"--offload-arch={ARCH}", "-munsafe-fp-atomics"] + common + ["-c", src, "-o", obj]
+    # host translation units (HIP runtime API only): compiled as host C++ by hipcc
+    return [_hipcc(), "-D__HIP_PLATFORM_AMD__"] + common + ["-c", src, "-o", obj]
+
+
+def _compile(src, obj, stamp):
+    cmd = _compile_cmd(src, obj)
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    _write_stamp(obj, stamp)
     return obj
 
 
@@ -55,38 +80,37 @@ def build(verbose=False):
     os.makedirs(OUT, exist_ok=True)
     srcs = sorted(glob.glob(os.path.join(CSRC, "*.cpp")) + glob.glob(os.path.join(CSRC, "*.hip")))
     hdrs = _headers()
-    jobs = []
-    objs = []
-    # a library newer than every source and header is current even when its objects are absent
-    # (they are gpurun-ignored, so the GPU box gets the .so alone)
-    lib_current = not _stale(LIB, srcs + hdrs)
-    for s in srcs:
-        if lib_current:
-            break
-        o = os.path.join(OUT, os.path.basename(s) + ".o")
-        objs.append(o)
-        if _stale(o, [s] + hdrs):
-            jobs.append((s, o))
-    if jobs:
-        with concurrent.futures.ThreadPoolExecutor(max_workers=min(8, len(jobs))) as ex:
-            for o in ex.map(lambda j: _compile(*j), jobs):
-                if verbose:
-                    print("built", os.path.relpath(o, REPO))
-    if not lib_current and _stale(LIB, objs):
-        cmd = [_hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", LIB] + objs + ["-lpthread"]
-        r = subprocess.run(cmd, capture_output=True, text=True)
+    objs = [os.path.join(OUT, os.path.basename(s) + ".o") for s in srcs]
+    link_cmd = [_hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", LIB] + objs + ["-lpthread"]
+    lib_stamp = _digest(srcs + hdrs, [_compile_cmd(s, o) for s, o in zip(srcs, objs)] + [link_cmd])
+    if not _current(LIB, lib_stamp):
+        jobs = []
+        for s, o in zip(srcs, objs):
+            st = _digest([s] + hdrs, [_compile_cmd(s, o)])
+            if not _current(o, st):
+                jobs.append((s, o, st))
+        if jobs:
+            with concurrent.futures.ThreadPoolExecutor(max_workers=min(8, len(jobs))) as ex:
+                for o in ex.map(lambda j: _compile(*j), jobs):
+                    if verbose:
+                        print("built", os.path.relpath(o, REPO))
+        r = subprocess.run(link_cmd, capture_output=True, text=True)
         if r.returncode != 0:
-            raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+            raise RuntimeError(f"link failed: {' '.join(link_cmd)}\n{r.stdout}\n{r.stderr}")
+        _write_stamp(LIB, lib_stamp)
         if verbose:
             print("linked", os.path.relpath(LIB, REPO))
     # the reference CLI sample rebuilt against the drop-in header (include/mp2v_decoder.h)
     cli_src = os.path.join(REPO, "tools", "tiny_mp2v_dec_gpu.cpp")
-    if os.path.exists(cli_src) and _stale(CLI, [cli_src, LIB] + hdrs):
+    if os.path.exists(cli_src):
         cmd = ["g++", "-std=c++17", "-O2", "-I", os.path.join(REPO, "include"), cli_src, "-o", CLI, "-L", OUT,
                "-lmp2vg", "-Wl,-rpath,$ORIGIN"]
-        r = subprocess.run(cmd, capture_output=True, text=True)
-        if r.returncode != 0:
-            raise RuntimeError(f"cli build failed: {' '.join(cmd)}\n{r.stderr}")
+        st = _digest([cli_src] + hdrs, [cmd]) + lib_stamp
+        if not _current(CLI, st):
+            r = subprocess.run(cmd, capture_output=True, text=True)
+            if r.returncode != 0:
+                raise RuntimeError(f"cli build failed: {' '.join(cmd)}\n{r.stderr}")
+            _write_stamp(CLI, st)
     return LIB
 
 

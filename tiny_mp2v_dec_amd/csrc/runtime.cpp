@@ -45,7 +45,11 @@ static constexpr size_t kStageBytes = 32u << 20;
 static constexpr size_t kMbPad = 16;  // >= the kernel's MB group size
 // independent picture sets per batch, one stream each (c2: 1 set 2.575 ms, 2 sets 2.502-2.535 ms,
 // 3 sets 2.566, 4 sets 2.590; MP2VG_STREAMS overrides for measurements)
-static const int kStreams = getenv("MP2VG_STREAMS") ? std::max(1, atoi(getenv("MP2VG_STREAMS"))) : 2;
+static int default_streams(const mp2vg_config_t* cfg) {
+    if (cfg->reserved & MP2VG_CTX_ONE_STREAM) return 1;
+    const char* e = getenv("MP2VG_STREAMS");
+    return e ? std::max(1, atoi(e)) : 2;
+}
 
 // One resident record batch.  The context keeps two, so the upload of batch k+1 (on the copy
 // stream) overlaps the decode of batch k; an upload waits only for the decode that last read
@@ -75,6 +79,7 @@ struct mp2vg_ctx {
     std::vector<hipEvent_t> sev;        // end of each set's launches
     uint8_t* d_pool = nullptr;
     int32_t nslots = 0;
+    int nstreams = 2;  // independent picture sets per batch (default_streams)
 
     Bank bank[2];
     int cur = -1;  // bank of the last upload
@@ -151,6 +156,7 @@ extern "C" int mp2vg_create(const mp2vg_config_t* cfg, mp2vg_ctx_t** out) {
     mp2vg_ctx_t* c = new mp2vg_ctx_t();
     c->cfg = *cfg;
     c->g.init(cfg->width, cfg->height, cfg->chroma_format);
+    c->nstreams = default_streams(cfg);
     bool ok = true;
     for (Bank& b : c->bank)
         ok = ok && hipEventCreateWithFlags(&b.uploaded, hipEventDisableTiming) == hipSuccess &&
@@ -265,6 +271,12 @@ static int plan_batch(mp2vg_ctx_t* c, const mp2vg_picture_t* pics, int32_t npics
                     return "coefficient words of a macroblock row are not contiguous";
             }
             if (m.cbp >> nb) return "cbp names a block the chroma format does not have";
+            // 4:4:4 field DCT: the reference places blocks 10/11 at (dct_type ? 1 : 8) * stride + 8
+            // with the doubled LUMA stride (mb_decoder.cpp:193-194), i.e. two rows down and one
+            // row into the next MB row, leaving odd rows unwritten; the parser rejects such
+            // streams, and no record producer may hand them to the kernel (spec placement)
+            if (nb == 12 && (m.flags & MP2VG_MB_DCT_FIELD) && m.cbp)
+                return "4:4:4 field-DCT macroblock (reference block 10/11 placement is unsupported)";
             if (!(m.flags & MP2VG_MB_INTRA)) {
                 uses[0] |= (m.flags & MP2VG_MB_FWD) || !(m.flags & MP2VG_MB_BWD);
                 uses[1] |= (m.flags & MP2VG_MB_BWD) != 0;
@@ -311,9 +323,9 @@ static int plan_batch(mp2vg_ctx_t* c, const mp2vg_picture_t* pics, int32_t npics
     //
     // Independent picture sets run on separate streams: pictures that touch a common slot (as
     // destination or used reference) are one component; components (closed GOPs) are dealt to
-    // kStreams sets, each with its own chain of level launches.  The streams run freely, so one
+    // c->nstreams sets, each with its own chain of level launches.  The streams run freely, so one
     // set's VALU-heavy I level overlaps another's memory-heavy B level and fills its launch tails.
-    const int nsets = std::max(1, std::min(kStreams, npics));
+    const int nsets = std::max(1, std::min(c->nstreams, npics));
     std::vector<int> parent(npics);
     for (int p = 0; p < npics; p++) parent[p] = p;
     auto find = [&](int x) {
@@ -421,6 +433,30 @@ static int batch_upload(mp2vg_ctx_t* c, const mp2vg_picture_t* pics, int32_t npi
     b.npics = npics;
     c->cur = k;
     c->batch_ready = true;
+    return MP2VG_OK;
+}
+
+extern "C" int mp2vg_batch_validate(const mp2vg_config_t* cfg, int32_t nslots, const mp2vg_picture_t* pics,
+                                    int32_t npics, const mp2vg_mb_t* mbs, uint64_t nmbs, const uint32_t* coefs,
+                                    uint64_t ncoefs, int32_t* nlaunches, int32_t* launch_of_pic,
+                                    int32_t* launch_mode, int32_t max_launches) {
+    if (!cfg || nslots <= 0 || !pics || npics <= 0 || !mbs || (!coefs && ncoefs)) return MP2VG_E_INVALID;
+    if (mp2vg_frame_geometry(cfg, nullptr, nullptr, nullptr, nullptr) != MP2VG_OK) return MP2VG_E_INVALID;
+    // a host-side shell of a context: plan_batch reads only the geometry and the slot count
+    mp2vg_ctx_t shell;
+    shell.cfg = *cfg;
+    shell.g.init(cfg->width, cfg->height, cfg->chroma_format);
+    shell.nslots = nslots;
+    shell.nstreams = default_streams(cfg);
+    std::vector<SliceDesc> slices;
+    std::vector<Launch> lb;
+    const int rc = plan_batch(&shell, pics, npics, mbs, nmbs, coefs, ncoefs, slices, lb);
+    if (rc != MP2VG_OK) return rc;
+    if (nlaunches) *nlaunches = (int32_t)lb.size();
+    for (size_t i = 0; i < lb.size(); i++) {
+        if (launch_mode && (int32_t)i < max_launches) launch_mode[i] = lb[i].mcm;
+        for (uint32_t k = lb[i].begin; launch_of_pic && k < lb[i].end; k++) launch_of_pic[slices[k].pic] = (int32_t)i;
+    }
     return MP2VG_OK;
 }
 
@@ -568,6 +604,21 @@ extern "C" int mp2vg_download_slot(mp2vg_ctx_t* c, int32_t slot, uint8_t* dst[3]
         const uint8_t* src = c->d_pool + (size_t)slot * c->g.slot_bytes + c->g.plane_off[p];
         HIPCHK(hipMemcpy2DAsync(dst[p], ds, src, c->g.stride[p], c->g.pw[p], c->g.ph[p], hipMemcpyDeviceToHost,
                                 c->stream));
+    }
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return MP2VG_OK;
+}
+
+extern "C" int mp2vg_copy_slot_packed(mp2vg_ctx_t* c, int32_t slot, void* dst, int32_t dst_on_device) {
+    if (!c || !dst || slot < 0 || slot >= c->nslots) return MP2VG_E_INVALID;
+    HIPCHK(hipSetDevice(c->cfg.device));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    uint8_t* d = (uint8_t*)dst;
+    const hipMemcpyKind kind = dst_on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+    for (int p = 0; p < 3; p++) {
+        const uint8_t* src = c->d_pool + (size_t)slot * c->g.slot_bytes + c->g.plane_off[p];
+        HIPCHK(hipMemcpy2DAsync(d, c->g.pw[p], src, c->g.stride[p], c->g.pw[p], c->g.ph[p], kind, c->stream));
+        d += (size_t)c->g.pw[p] * c->g.ph[p];
     }
     HIPCHK(hipStreamSynchronize(c->stream));
     return MP2VG_OK;

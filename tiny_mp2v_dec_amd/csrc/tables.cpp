@@ -233,4 +233,66 @@ int mp2vg_frame_geometry(const mp2vg_config_t* cfg, int32_t width[3], int32_t he
     return MP2VG_OK;
 }
 
+// Conformance hook: one code through the host emitter's own Annex B decoders (the LUTs parse.cpp
+// uses), for the per-entry VLC tests against the reference's decoders (tests/test_vlc.py).
+int mp2vg_vlc_decode(int32_t table, uint64_t bits, int32_t* value, int32_t* aux, int32_t* consumed) {
+    using namespace mp2vg;
+    if (!value || !aux || !consumed) return MP2VG_E_INVALID;
+    uint8_t buf[16] = {};
+    for (int i = 0; i < 8; i++) buf[i] = (uint8_t)(bits >> (56 - 8 * i));
+    BitReader br(buf, buf + sizeof buf);
+    const Tables& T = Tables::get();
+    *aux = 0;
+    int idx = -1;
+    switch (table) {
+    case MP2VG_VLC_MBA:
+        idx = T.mba.decode(br);
+        *value = idx == 100 ? -33 : (idx >= 0 ? kMbaCodes[idx].a : 0);  // escape: +33 to the next code
+        break;
+    case MP2VG_VLC_MBTYPE_I:
+    case MP2VG_VLC_MBTYPE_P:
+    case MP2VG_VLC_MBTYPE_B: {
+        const int pct = table - MP2VG_VLC_MBTYPE_I + 1;
+        idx = T.mbtype[pct].decode(br);
+        if (idx >= 0) *value = (int32_t)(pct == 1 ? kMbTypeI : pct == 2 ? kMbTypeP : kMbTypeB)[idx].a;
+        break;
+    }
+    case MP2VG_VLC_CBP:
+        idx = T.cbp.decode(br);
+        if (idx >= 0) *value = kCbpCodes[idx].a;
+        break;
+    case MP2VG_VLC_MOTION:  // magnitude, then the sign bit of a non-zero code (mb_decoder.cpp:479-519)
+        idx = T.motion.decode(br);
+        if (idx >= 0) {
+            int mc = kMotionCodes[idx].a;
+            if (mc && br.read(1)) mc = -mc;
+            *value = mc;
+        }
+        break;
+    case MP2VG_VLC_DC_LUMA:
+    case MP2VG_VLC_DC_CHROMA:
+        idx = (table == MP2VG_VLC_DC_LUMA ? T.dc_luma : T.dc_chroma).decode(br);
+        if (idx >= 0) *value = (table == MP2VG_VLC_DC_LUMA ? kDcSizeLuma : kDcSizeChroma)[idx].a;
+        break;
+    case MP2VG_VLC_COEF_B14:
+    case MP2VG_VLC_COEF_B15: {  // run, signed level (sign bit / escape fields consumed); EOB: run -1
+        int run = 0, level = 0;
+        const int kind = T.coefs[table - MP2VG_VLC_COEF_B14].decode(br, run, level);
+        idx = kind < 0 ? -1 : 0;
+        *value = kind == CoefLut::EOB ? -1 : run;
+        *aux = level;
+        break;
+    }
+    default:
+        set_error("mp2vg_vlc_decode: no decoder for this table (dual-prime dmvector is unsupported)");
+        return MP2VG_E_UNSUPPORTED;
+    }
+    *consumed = (int32_t)br.bitpos();
+    if (idx < 0) {
+        set_error("mp2vg_vlc_decode: invalid code");
+        return MP2VG_E_BITSTREAM;
+    }
+    return MP2VG_OK;
+}
+
 }  // extern "C"

@@ -71,12 +71,40 @@ class Parsed:
         return len(self.pics)
 
 
+def plan_batch(width, height, chroma_format, nslots, pics, mbs, coefs, one_stream=False):
+    """mp2vg_batch_validate: the upload's host-side record validation and launch planning, with no
+    device.  Returns (launch index of each picture, kernel mode of each launch: 0 I, 1 P, 2 B,
+    3 mixed); raises Mp2vgError for a batch the upload would refuse."""
+    cfg = _lib.make_config(width, height, chroma_format, pool=nslots,
+                           flags=_lib.MP2VG_CTX_ONE_STREAM if one_stream else 0)
+    pics = np.ascontiguousarray(pics, PIC_DTYPE)
+    mbs = np.ascontiguousarray(mbs, MB_DTYPE)
+    coefs = np.ascontiguousarray(coefs, np.uint32)
+    vp = ctypes.c_void_p
+    n = ctypes.c_int32()
+    of_pic = np.zeros(len(pics), np.int32)
+    mode = np.zeros(4096, np.int32)
+    i32p = ctypes.POINTER(ctypes.c_int32)
+    check(lib().mp2vg_batch_validate(ctypes.byref(cfg), nslots, pics.ctypes.data_as(vp), len(pics),
+                                     mbs.ctypes.data_as(vp), len(mbs),
+                                     coefs.ctypes.data_as(vp) if len(coefs) else None, len(coefs),
+                                     ctypes.byref(n), of_pic.ctypes.data_as(i32p), mode.ctypes.data_as(i32p),
+                                     len(mode)), "batch_validate")
+    return of_pic, mode[:min(n.value, len(mode))].copy()
+
+
+def validate_batch(width, height, chroma_format, nslots, pics, mbs, coefs):
+    """Number of kernel launches of a valid batch (plan_batch); raises Mp2vgError otherwise."""
+    return len(plan_batch(width, height, chroma_format, nslots, pics, mbs, coefs)[1])
+
+
 class DeviceContext:
     """mp2vg_ctx_t: a frame pool in HBM plus a resident record batch on one GPU."""
 
-    def __init__(self, width, height, chroma_format, slots, device=0):
+    def __init__(self, width, height, chroma_format, slots, device=0, one_stream=False):
         self.width, self.height, self.chroma_format = width, height, chroma_format
-        self.cfg = _lib.make_config(width, height, chroma_format, pool=slots, device=device)
+        self.cfg = _lib.make_config(width, height, chroma_format, pool=slots, device=device,
+                                    flags=_lib.MP2VG_CTX_ONE_STREAM if one_stream else 0)
         self.h = ctypes.c_void_p()
         check(lib().mp2vg_create(ctypes.byref(self.cfg), ctypes.byref(self.h)), "create")
         self.pw, self.ph, self.stride, self.slot_bytes = _lib.geometry(width, height, chroma_format)
@@ -144,6 +172,16 @@ class DeviceContext:
         ptrs = (ctypes.c_void_p * 3)(*[p.ctypes.data for p in planes])
         check(lib().mp2vg_download_slot(self.h, slot, ptrs, None), "download_slot")
         return planes
+
+    def frame_bytes(self):
+        """Bytes of one frame in the packed write_yuv layout (Y, U, V visible planes)."""
+        return sum(self.pw[i] * self.ph[i] for i in range(3))
+
+    def copy_packed(self, slot, dst_ptr, on_device):
+        """Visible planes of `slot`, packed Y|U|V, into dst_ptr (HBM of this context's device when
+        on_device, e.g. a torch tensor's data_ptr(); else host memory)."""
+        check(lib().mp2vg_copy_slot_packed(self.h, int(slot), ctypes.c_void_p(dst_ptr), 1 if on_device else 0),
+              "copy_slot_packed")
 
     def digests(self, slots):
         slots = np.ascontiguousarray(slots, np.int32)
