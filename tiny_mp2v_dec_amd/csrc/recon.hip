@@ -341,8 +341,25 @@ __device__ __forceinline__ void tap_issue(Tap<NW>& t, bool use, __amdgpu_buffer_
     // dword-aligned row start: byte-exact (unaligned) buffer loads would save two alignbytes per
     // dword but cost twice the texture-address cycles, a net loss (tools/unaligned_check.hip)
     const uint32_t row = plane_off + (uint32_t)(Xc & ~3);
-    const uint32_t o0 = (use && !(ABL & 32)) ? row + mul24_asm((uint32_t)Y0, (uint32_t)stride) : kNoTap;
-    const uint32_t o1 = (use && hy && edge && !(ABL & 32)) ? row + mul24_asm((uint32_t)Y1, (uint32_t)stride) : kNoTap;
+    uint32_t o0 = (use && !(ABL & 32)) ? row + mul24_asm((uint32_t)Y0, (uint32_t)stride) : kNoTap;
+    uint32_t o1 = (use && hy && edge && !(ABL & 32)) ? row + mul24_asm((uint32_t)Y1, (uint32_t)stride) : kNoTap;
+    if (ABL & 1024) {  // dev ablation (timing only): apron-tiled addresses, 128-B tiles of 4 x 32 B
+        const uint32_t A = (uint32_t)(Xc & ~3);  // luma (4 rows x 32 B) / chroma (8 rows x 16 B)
+        const uint32_t ncol = (uint32_t)stride >> (plane == 0 ? 4 : 3);
+        auto toff = [&](int yy) -> uint32_t {
+            const uint32_t y = (uint32_t)yy;
+            if (plane == 0)
+                return ((mul24_asm(y >> 2, ncol) + (A >> 4)) * 128u + (y & 3u) * 32u + (A & 12u)) & 0x1FFFFFu;
+            return 0x200000u + (uint32_t)(plane - 1) * 0x70000u +
+                   (((mul24_asm(y >> 3, ncol) + (A >> 3)) * 128u + (y & 7u) * 16u + (A & 4u)) & 0x7FFFFu);
+        };
+        o0 = use ? toff(Y0) : kNoTap;
+        o1 = (use && hy && edge) ? toff(Y1) : kNoTap;
+    }
+    if (ABL & 2048) {  // dev ablation (timing only): every tap inside a 64-KB window (L1/L2 hits)
+        o0 = o0 == kNoTap ? kNoTap : (o0 & 0xFFFFu);
+        o1 = o1 == kNoTap ? kNoTap : (o1 & 0xFFFFu);
+    }
     load_row<NW, ABL>(t.a, ref, o0);
     if (!(ABL & 512)) load_row<NW, ABL>(t.b, ref, o1);  // (dev ablation 512: no edge-row loads)
     else for (int i = 0; i <= NW; i++) t.b[i] = 0;
@@ -495,6 +512,9 @@ __device__ __forceinline__ void store_pass(uint32_t r0, uint32_t r1, bool live, 
     dst = live ? dst : wsink;  // branch-free: every lane stores (see Tap)
     if (ABL & 8) {
         asm volatile("" ::"v"(out[0]), "v"(out[1]), "v"(out[2]), "v"(out[3]), "v"(dst));
+    } else if (ABL & 4096) {  // dev ablation (timing only): one dword per row store (1/4, 1/2 bytes)
+        asm volatile("" ::"v"(out[0]), "v"(out[1]), "v"(out[2]), "v"(out[3]));
+        *(uint32_t*)dst = out[0] ^ out[1] ^ (NW == 4 ? out[2] ^ out[3] : 0u);
     } else if (NW == 4) {
         *(uint4*)dst = make_uint4(out[0], out[1], out[2], out[3]);
     } else {
@@ -942,6 +962,12 @@ hipError_t launch_recon(int cf, int mcm, const KArgs& a, hipStream_t stream) {
         case 96: return launch_mcm<1, 96>(mcm, a, g, stream);
         case 128: return launch_mcm<1, 128>(mcm, a, g, stream);
         case 512: return launch_mcm<1, 512>(mcm, a, g, stream);
+        case 1024: return launch_mcm<1, 1024>(mcm, a, g, stream);
+        case 1032: return launch_mcm<1, 1032>(mcm, a, g, stream);
+        case 2048: return launch_mcm<1, 2048>(mcm, a, g, stream);
+        case 2056: return launch_mcm<1, 2056>(mcm, a, g, stream);
+        case 3072: return launch_mcm<1, 3072>(mcm, a, g, stream);
+        case 4096: return launch_mcm<1, 4096>(mcm, a, g, stream);
         default: return hipErrorInvalidValue;
         }
     }

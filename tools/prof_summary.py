@@ -34,7 +34,9 @@ def main():
     ap.add_argument("tag")
     ap.add_argument("--out")
     ap.add_argument("--json", help="write HBM traffic per bench step (bytes) for bench.py's roofline.traffic")
-    ap.add_argument("--steps-total", type=int, default=12, help="bench steps + warmup steps profiled")
+    ap.add_argument("--steps-total", type=int, default=18,
+                    help="batches the profiled bench run decodes: steps + warmup + the 6 batches of its one-stream "
+                         "per-kernel context (bench.py: 10 + 2 + 6 by default)")
     ap.add_argument("--config", default="c2")
     ap.add_argument("--gops", type=int, default=64)
     args = ap.parse_args()
