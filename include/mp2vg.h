@@ -189,6 +189,49 @@ int  mp2vg_slot_device_ptr(mp2vg_ctx_t* ctx, int32_t slot, void** dptr);
  * tiny_mp2v_dec_amd.records.planes_digest) */
 int  mp2vg_slot_digests(mp2vg_ctx_t* ctx, const int32_t* slots, int32_t n, uint64_t* out);
 
+/* ---- stream headers ----------------------------------------------------------------------
+ * The sequence-level headers the reference keeps as public members of mp2v_decoder_c
+ * (decoder.h:124-130), with the reference's field names (mp2v_hdr.h:61-141) and parsed the way
+ * the reference parses them (mp2v_hdr.cpp:4-83): a later header of the same kind overwrites an
+ * earlier one, the matrices are the 64 bytes as transmitted, fields a header does not carry stay
+ * 0, and the start-code fields hold the 32-bit start code (extension_start_code stays 0, as the
+ * reference never sets it).  Scalable extensions are outside the decodable subset (rejected). */
+typedef struct mp2vg_sequence_header {
+    uint32_t sequence_header_code, horizontal_size_value, vertical_size_value, aspect_ratio_information,
+             frame_rate_code, bit_rate_value, vbv_buffer_size_value, constrained_parameters_flag,
+             load_intra_quantiser_matrix;
+    uint8_t  intra_quantiser_matrix[64];
+    uint32_t load_non_intra_quantiser_matrix;
+    uint8_t  non_intra_quantiser_matrix[64];
+} mp2vg_sequence_header_t;
+typedef struct mp2vg_sequence_extension {
+    uint32_t extension_start_code, extension_start_code_identifier, profile_and_level_indication,
+             progressive_sequence, chroma_format, horizontal_size_extension, vertical_size_extension,
+             bit_rate_extension, vbv_buffer_size_extension, low_delay, frame_rate_extension_n,
+             frame_rate_extension_d;
+} mp2vg_sequence_extension_t;
+typedef struct mp2vg_sequence_display_extension {
+    uint32_t extension_start_code_identifier, video_format, colour_description, colour_primaries,
+             transfer_characteristics, matrix_coefficients, display_horizontal_size, display_vertical_size;
+} mp2vg_sequence_display_extension_t;
+typedef struct mp2vg_sequence_scalable_extension {
+    uint32_t extension_start_code_identifier, scalable_mode, layer_id, lower_layer_prediction_horizontal_size,
+             lower_layer_prediction_vertical_size, horizontal_subsampling_factor_m,
+             horizontal_subsampling_factor_n, vertical_subsampling_factor_m, vertical_subsampling_factor_n,
+             picture_mux_enable, mux_to_progressive_sequence, picture_mux_order, picture_mux_factor;
+} mp2vg_sequence_scalable_extension_t;
+typedef struct mp2vg_group_of_pictures_header {
+    uint32_t group_start_code, time_code, closed_gop, broken_link;
+} mp2vg_group_of_pictures_header_t;
+typedef struct mp2vg_stream_headers {
+    int32_t have_sequence_display_extension;  /* reference: m_sequence_display_extension != nullptr */
+    int32_t have_group_of_pictures_header;    /* reference: m_group_of_pictures_header != nullptr   */
+    mp2vg_sequence_header_t sequence_header;
+    mp2vg_sequence_extension_t sequence_extension;
+    mp2vg_sequence_display_extension_t sequence_display_extension;
+    mp2vg_group_of_pictures_header_t group_of_pictures_header; /* the last one in the stream      */
+} mp2vg_stream_headers_t;
+
 /* ---- host record emitter -------------------------------------------------------------- */
 typedef struct mp2vg_parsed mp2vg_parsed_t;
 
@@ -206,6 +249,18 @@ const uint32_t*        mp2vg_parsed_coefs(const mp2vg_parsed_t* p);
 int  mp2vg_parsed_display_order(const mp2vg_parsed_t* p, int32_t* order, int32_t n);
 /* GOP index (0-based, by group_start_code) of each picture, for GOP sharding */
 int  mp2vg_parsed_gop_index(const mp2vg_parsed_t* p, int32_t* gop, int32_t n);
+/* sequence headers of the parsed stream (see mp2vg_stream_headers_t) */
+int  mp2vg_parsed_stream_headers(const mp2vg_parsed_t* p, mp2vg_stream_headers_t* out);
+/* Independent shards for GOP sharding: shard[i] of each picture (decode order), numbered from 0.
+ * A shard is a maximal run of pictures, in decode order, that no later picture predicts across:
+ * a closed GOP (or several open GOPs chained by their leading B pictures), since a picture's
+ * references are only the two latest anchors (reference decoder.cpp:299-304).  The B pictures
+ * between the first two anchors of a GOP whose header has closed_gop = 1 predict backward only
+ * (ISO/IEC 13818-2 6.3.8), so their picture-level forward anchor (the previous GOP's last one,
+ * reference decoder.cpp:299-304) does not join the shards; the multi-device decoder refuses
+ * (MP2VG_E_UNSUPPORTED) such a picture if a macroblock of it does predict forward.  Returns the
+ * number of shards. */
+int  mp2vg_parsed_shards(const mp2vg_parsed_t* p, int32_t* shard, int32_t n);
 void mp2vg_parsed_free(mp2vg_parsed_t* p);
 
 /* Conformance hook: decode one Annex B code (MSB-first 64-bit window: the code, then whatever
@@ -254,15 +309,34 @@ typedef struct mp2vg_frame {
     int32_t  width[3], height[3], stride[3];
     int32_t  picture_coding_type;
     int32_t  decode_index;
+    int32_t  device;          /* HIP device that decoded the frame (its planes' device with
+                                 MP2VG_DECODER_DEVICE_FRAMES)                                 */
 } mp2vg_frame_t;
 typedef void (*mp2vg_render_fn)(void* user, const mp2vg_frame_t* frame);
 typedef struct mp2vg_decoder mp2vg_decoder_t;
 
 int  mp2vg_decoder_create(const mp2vg_config_t* cfg, mp2vg_render_fn fn, void* user,
                           mp2vg_decoder_t** out);
+/* The drop-in decoder over several devices (GOP sharding): the independent shards of a stream
+ * (mp2vg_parsed_shards) are dealt round-robin, shard s -> devices[s % ndevices], each device
+ * decoding its shards with its own frame pool, record banks and streams, concurrently; frames
+ * reach the renderer in the stream's display order whatever device decoded them.  cfg->device is
+ * ignored; a device may be listed more than once (e.g. {0, 0}: two independent lanes on one GPU).
+ * The reference's picture-parallel runtime this replaces: threads.cpp:22-36, 120-186 and
+ * decoder.cpp:299-304, 346-379.  ndevices = 1 is mp2vg_decoder_create on devices[0]. */
+int  mp2vg_decoder_create_multi(const mp2vg_config_t* cfg, const int32_t* devices, int32_t ndevices,
+                                mp2vg_render_fn fn, void* user, mp2vg_decoder_t** out);
 /* decode a whole elementary stream (reference decode(): single-shot, synchronous; frames are
  * delivered in display order to fn on a dedicated render thread before this returns) */
 int  mp2vg_decoder_decode(mp2vg_decoder_t* dec, const uint8_t* buf, uint64_t len);
+/* sequence headers of the last decoded stream (reference public members, decoder.h:124-130) */
+int  mp2vg_decoder_stream_headers(const mp2vg_decoder_t* dec, mp2vg_stream_headers_t* out);
+/* frames decoded by each lane of the decoder in its last decode() (lane i = devices[i]); returns
+ * the number of lanes */
+int  mp2vg_decoder_lane_frames(const mp2vg_decoder_t* dec, int32_t* frames, int32_t n);
+/* frame buffers the decoder's frame pools hold (host + device): 2 * 16 + 4 per lane unless a
+ * renderer that holds no frame had to wait for display order (then the pool grows) */
+int  mp2vg_decoder_frames_allocated(const mp2vg_decoder_t* dec);
 int  mp2vg_decoder_destroy(mp2vg_decoder_t* dec);
 
 #ifdef __cplusplus

@@ -10,6 +10,9 @@
 // usage: ref_decode <in.m2v> <width> <height> <chroma_format 1|2|3> <threads> <out.yuv|-> [repeat]
 //   out "-" : decode without writing (timing mode).
 //   out "*.dig" : write one uint64 frame digest per frame in display order instead of the YUV.
+//   out "*.hdr.json" : after decode(), write the decoder's public header members (reference
+//                      decoder.h:124-130: m_sequence_header, m_sequence_extension,
+//                      m_sequence_display_extension, m_group_of_pictures_header, user_data) as JSON.
 // prints one JSON line: {"frames": F, "ms": best-of-repeat decode() wall time, "threads": T}
 #include <chrono>
 #include <cstdio>
@@ -49,6 +52,55 @@ static uint64_t frame_digest(frame_c* frame) {
     return acc;
 }
 
+static void put_matrix(FILE* fp, const char* name, const uint8_t* m) {
+    fprintf(fp, "\"%s\": [", name);
+    for (int i = 0; i < 64; i++) fprintf(fp, "%s%u", i ? ", " : "", m[i]);
+    fprintf(fp, "]");
+}
+
+static void write_headers(FILE* fp, mp2v_decoder_c& dec) {
+    const sequence_header_t& sh = dec.m_sequence_header;
+    fprintf(fp, "{\"sequence_header\": {\"sequence_header_code\": %u, \"horizontal_size_value\": %u, "
+                "\"vertical_size_value\": %u, \"aspect_ratio_information\": %u, \"frame_rate_code\": %u, "
+                "\"bit_rate_value\": %u, \"vbv_buffer_size_value\": %u, \"constrained_parameters_flag\": %u, "
+                "\"load_intra_quantiser_matrix\": %u, \"load_non_intra_quantiser_matrix\": %u, ",
+            sh.sequence_header_code, sh.horizontal_size_value, sh.vertical_size_value, sh.aspect_ratio_information,
+            sh.frame_rate_code, sh.bit_rate_value, sh.vbv_buffer_size_value, sh.constrained_parameters_flag,
+            sh.load_intra_quantiser_matrix, sh.load_non_intra_quantiser_matrix);
+    // the matrices only when loaded (the reference leaves them uninitialised otherwise)
+    if (sh.load_intra_quantiser_matrix) { put_matrix(fp, "intra_quantiser_matrix", sh.intra_quantiser_matrix); fprintf(fp, ", "); }
+    if (sh.load_non_intra_quantiser_matrix) { put_matrix(fp, "non_intra_quantiser_matrix", sh.non_intra_quantiser_matrix); fprintf(fp, ", "); }
+    fprintf(fp, "\"_\": 0}, ");
+    const sequence_extension_t& se = dec.m_sequence_extension;
+    fprintf(fp, "\"sequence_extension\": {\"extension_start_code\": %u, \"extension_start_code_identifier\": %u, "
+                "\"profile_and_level_indication\": %u, \"progressive_sequence\": %u, \"chroma_format\": %u, "
+                "\"horizontal_size_extension\": %u, \"vertical_size_extension\": %u, \"bit_rate_extension\": %u, "
+                "\"vbv_buffer_size_extension\": %u, \"low_delay\": %u, \"frame_rate_extension_n\": %u, "
+                "\"frame_rate_extension_d\": %u}, ",
+            se.extension_start_code, se.extension_start_code_identifier, se.profile_and_level_indication,
+            se.progressive_sequence, se.chroma_format, se.horizontal_size_extension, se.vertical_size_extension,
+            se.bit_rate_extension, se.vbv_buffer_size_extension, se.low_delay, se.frame_rate_extension_n,
+            se.frame_rate_extension_d);
+    if (const sequence_display_extension_t* de = dec.m_sequence_display_extension)
+        fprintf(fp, "\"sequence_display_extension\": {\"extension_start_code_identifier\": %u, \"video_format\": %u, "
+                    "\"colour_description\": %u, \"colour_primaries\": %u, \"transfer_characteristics\": %u, "
+                    "\"matrix_coefficients\": %u, \"display_horizontal_size\": %u, \"display_vertical_size\": %u}, ",
+                de->extension_start_code_identifier, de->video_format, de->colour_description,
+                de->colour_description ? de->colour_primaries : 0, de->colour_description ? de->transfer_characteristics : 0,
+                de->colour_description ? de->matrix_coefficients : 0, de->display_horizontal_size,
+                de->display_vertical_size);
+    else
+        fprintf(fp, "\"sequence_display_extension\": null, ");
+    if (const group_of_pictures_header_t* gh = dec.m_group_of_pictures_header)
+        fprintf(fp, "\"group_of_pictures_header\": {\"group_start_code\": %u, \"time_code\": %u, \"closed_gop\": %u, "
+                    "\"broken_link\": %u}, ",
+                gh->group_start_code, gh->time_code, gh->closed_gop, gh->broken_link);
+    else
+        fprintf(fp, "\"group_of_pictures_header\": null, ");
+    fprintf(fp, "\"sequence_scalable_extension\": %s, \"user_data_len\": %zu}\n",
+            dec.m_sequence_scalable_extension ? "1" : "null", dec.user_data.size());
+}
+
 int main(int argc, char** argv) {
     if (argc < 7) {
         fprintf(stderr, "usage: %s in.m2v width height chroma_format threads out.yuv|- [repeat]\n", argv[0]);
@@ -79,6 +131,7 @@ int main(int argc, char** argv) {
     FILE* out = nullptr;
     const size_t olen = strlen(out_path);
     const bool digest = olen > 4 && !strcmp(out_path + olen - 4, ".dig");
+    const bool headers = olen > 9 && !strcmp(out_path + olen - 9, ".hdr.json");
     if (strcmp(out_path, "-") != 0) {
         out = fopen(out_path, "wb");
         if (!out) { perror(out_path); return 1; }
@@ -90,9 +143,10 @@ int main(int argc, char** argv) {
         FILE* fp = (r == 0) ? out : nullptr;
         auto t0 = std::chrono::steady_clock::now();
         {
-            mp2v_decoder_c dec(cfg, [fp, digest, &nframes](frame_c* f) {
+            mp2v_decoder_c dec(cfg, [fp, digest, headers, &nframes](frame_c* f) {
                 nframes++;
-                if (fp && digest) {
+                if (headers) {
+                } else if (fp && digest) {
                     const uint64_t d = frame_digest(f);
                     fwrite(&d, sizeof d, 1, fp);
                 } else if (fp) {
@@ -100,6 +154,11 @@ int main(int argc, char** argv) {
                 }
             });
             dec.decode(buf.data(), (int)padded);
+            if (fp && headers) {
+                // decode() only queues the pictures: the headers are final once it returns, the
+                // frames once the destructor has joined the threads
+                write_headers(fp, dec);
+            }
         }  // destructor joins the render + worker threads: all frames delivered
         auto t1 = std::chrono::steady_clock::now();
         double ms = std::chrono::duration<double, std::milli>(t1 - t0).count();

@@ -64,7 +64,43 @@ class GenParams(ctypes.Structure):
 class Frame(ctypes.Structure):
     _fields_ = [("planes", ctypes.POINTER(ctypes.c_uint8) * 3), ("width", ctypes.c_int32 * 3),
                 ("height", ctypes.c_int32 * 3), ("stride", ctypes.c_int32 * 3),
-                ("picture_coding_type", ctypes.c_int32), ("decode_index", ctypes.c_int32)]
+                ("picture_coding_type", ctypes.c_int32), ("decode_index", ctypes.c_int32),
+                ("device", ctypes.c_int32)]
+
+
+class SequenceHeader(ctypes.Structure):  # mp2vg_sequence_header_t (reference mp2v_hdr.h:61-75)
+    _fields_ = [(n, ctypes.c_uint32) for n in (
+        "sequence_header_code", "horizontal_size_value", "vertical_size_value", "aspect_ratio_information",
+        "frame_rate_code", "bit_rate_value", "vbv_buffer_size_value", "constrained_parameters_flag",
+        "load_intra_quantiser_matrix")] + [("intra_quantiser_matrix", ctypes.c_uint8 * 64),
+                                           ("load_non_intra_quantiser_matrix", ctypes.c_uint32),
+                                           ("non_intra_quantiser_matrix", ctypes.c_uint8 * 64)]
+
+
+class SequenceExtension(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint32) for n in (
+        "extension_start_code", "extension_start_code_identifier", "profile_and_level_indication",
+        "progressive_sequence", "chroma_format", "horizontal_size_extension", "vertical_size_extension",
+        "bit_rate_extension", "vbv_buffer_size_extension", "low_delay", "frame_rate_extension_n",
+        "frame_rate_extension_d")]
+
+
+class SequenceDisplayExtension(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint32) for n in (
+        "extension_start_code_identifier", "video_format", "colour_description", "colour_primaries",
+        "transfer_characteristics", "matrix_coefficients", "display_horizontal_size", "display_vertical_size")]
+
+
+class GopHeader(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint32) for n in ("group_start_code", "time_code", "closed_gop", "broken_link")]
+
+
+class StreamHeaders(ctypes.Structure):  # mp2vg_stream_headers_t
+    _fields_ = [("have_sequence_display_extension", ctypes.c_int32),
+                ("have_group_of_pictures_header", ctypes.c_int32),
+                ("sequence_header", SequenceHeader), ("sequence_extension", SequenceExtension),
+                ("sequence_display_extension", SequenceDisplayExtension),
+                ("group_of_pictures_header", GopHeader)]
 
 
 RENDER_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.POINTER(Frame))
@@ -75,9 +111,11 @@ EXPORTS = [
     "mp2vg_frame_geometry", "mp2vg_reserve_slots", "mp2vg_batch_upload", "mp2vg_batch_validate", "mp2vg_batch_decode",
     "mp2vg_synchronize", "mp2vg_last_launch_times", "mp2vg_last_batch_time", "mp2vg_batch_times", "mp2vg_download_slot", "mp2vg_copy_slot_packed", "mp2vg_slot_device_ptr",
     "mp2vg_slot_digests", "mp2vg_parse_es", "mp2vg_parsed_counts", "mp2vg_parsed_pictures", "mp2vg_parsed_mbs",
-    "mp2vg_parsed_coefs", "mp2vg_parsed_display_order", "mp2vg_parsed_gop_index", "mp2vg_parsed_free", "mp2vg_vlc_decode",
+    "mp2vg_parsed_coefs", "mp2vg_parsed_display_order", "mp2vg_parsed_gop_index", "mp2vg_parsed_stream_headers",
+    "mp2vg_parsed_shards", "mp2vg_parsed_free", "mp2vg_vlc_decode",
     "mp2vg_gen_default_params", "mp2vg_generate_es", "mp2vg_free", "mp2vg_decoder_create",
-    "mp2vg_decoder_decode", "mp2vg_decoder_destroy",
+    "mp2vg_decoder_create_multi", "mp2vg_decoder_decode", "mp2vg_decoder_stream_headers",
+    "mp2vg_decoder_lane_frames", "mp2vg_decoder_frames_allocated", "mp2vg_decoder_destroy",
 ]
 
 _lib = None
@@ -119,13 +157,19 @@ def lib():
         "mp2vg_parsed_coefs": ([VP], VP),
         "mp2vg_parsed_display_order": ([VP, P(I32), I32], ctypes.c_int),
         "mp2vg_parsed_gop_index": ([VP, P(I32), I32], ctypes.c_int),
+        "mp2vg_parsed_stream_headers": ([VP, P(StreamHeaders)], ctypes.c_int),
+        "mp2vg_parsed_shards": ([VP, P(I32), I32], ctypes.c_int),
         "mp2vg_parsed_free": ([VP], None),
         "mp2vg_vlc_decode": ([I32, U64, P(I32), P(I32), P(I32)], ctypes.c_int),
         "mp2vg_gen_default_params": ([P(GenParams)], None),
         "mp2vg_generate_es": ([P(GenParams), P(VP), P(U64)], ctypes.c_int),
         "mp2vg_free": ([VP], None),
         "mp2vg_decoder_create": ([P(Config), RENDER_FN, VP, P(VP)], ctypes.c_int),
+        "mp2vg_decoder_create_multi": ([P(Config), P(I32), I32, RENDER_FN, VP, P(VP)], ctypes.c_int),
         "mp2vg_decoder_decode": ([VP, VP, U64], ctypes.c_int),
+        "mp2vg_decoder_stream_headers": ([VP, P(StreamHeaders)], ctypes.c_int),
+        "mp2vg_decoder_lane_frames": ([VP, P(I32), I32], ctypes.c_int),
+        "mp2vg_decoder_frames_allocated": ([VP], ctypes.c_int),
         "mp2vg_decoder_destroy": ([VP], ctypes.c_int),
     }
     for name, (args, res) in sig.items():

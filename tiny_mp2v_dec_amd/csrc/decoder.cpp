@@ -15,6 +15,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <functional>
 #include <cstdlib>
 #include <condition_variable>
 #include <deque>
@@ -54,12 +57,19 @@ const int kDlStreams = getenv("MP2VG_DL_STREAMS") ? std::min(kMaxDl, std::max(1,
 struct HostFrame {
     uint8_t* data = nullptr;
     mp2vg_frame_t f;
+    class FramePool* owner = nullptr;
 };
 
+// A frame pool of `cap` frames.  The reference blocks its decoder on a fixed picture pool
+// (threads.cpp:164-166 wait_for_render / wait_for_free); here get() blocks while every frame is
+// out and the renderer still holds or has queued some (each put() wakes it).  Only when the
+// renderer has none -- the frames are all waiting for display order behind a picture that is
+// not decoded yet -- does the pool grow past cap, since waiting could never end.
 class FramePool {
   public:
-    FramePool(size_t bytes, bool device) : bytes_(bytes), device_(device) {}
+    FramePool(size_t bytes, bool device, int dev) : bytes_(bytes), device_(device), dev_(dev) {}
     ~FramePool() {
+        if (device_) hipSetDevice(dev_);
         for (HostFrame* f : all_) {
             if (device_)
                 hipFree(f->data);
@@ -69,6 +79,7 @@ class FramePool {
         }
     }
     bool reserve(int n) {
+        cap_ = std::max(cap_, n);
         while ((int)all_.size() < n) {
             HostFrame* f = alloc();
             if (!f) return false;
@@ -76,25 +87,39 @@ class FramePool {
         }
         return true;
     }
-    HostFrame* get() {
+    // renderer_holds(): frames queued for or inside the render callback (under no pool lock)
+    HostFrame* get(const std::function<int()>& renderer_holds) {
         {
-            std::lock_guard<std::mutex> lk(mu_);
-            if (!free_.empty()) {
-                HostFrame* f = free_.back();
-                free_.pop_back();
-                return f;
+            std::unique_lock<std::mutex> lk(mu_);
+            for (;;) {
+                if (!free_.empty()) {
+                    HostFrame* f = free_.back();
+                    free_.pop_back();
+                    return f;
+                }
+                if ((int)all_.size() < cap_ || renderer_holds() == 0) break;
+                cv_.wait_for(lk, std::chrono::milliseconds(20));
             }
         }
         return alloc();
     }
     void put(HostFrame* f) {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            free_.push_back(f);
+        }
+        cv_.notify_all();
+    }
+    size_t size() {
         std::lock_guard<std::mutex> lk(mu_);
-        free_.push_back(f);
+        return all_.size();
     }
 
   private:
     HostFrame* alloc() {
         auto* f = new HostFrame();
+        f->owner = this;
+        if (device_) hipSetDevice(dev_);
         const hipError_t e = device_ ? hipMalloc((void**)&f->data, bytes_)
                                      : hipHostMalloc((void**)&f->data, bytes_, hipHostMallocDefault);
         if (e != hipSuccess) {
@@ -107,7 +132,10 @@ class FramePool {
     }
     size_t bytes_;
     bool device_;
+    int dev_;
+    int cap_ = 0;
     std::mutex mu_;
+    std::condition_variable cv_;
     std::vector<HostFrame*> all_, free_;
 };
 
@@ -132,85 +160,154 @@ struct PinnedBuf {
         return true;
     }
 };
+
+// One device of the decoder (GOP sharding deals the stream's independent shards to lanes):
+// its own record context (frame slots, two record banks, launch streams), download streams,
+// and, with MP2VG_DECODER_DEVICE_FRAMES, its own HBM frame pool.
+struct Lane {
+    int device = 0;
+    mp2vg_ctx_t* ctx = nullptr;
+    int nslots = 0;
+    std::unique_ptr<FramePool> dpool;
+    PinnedBuf mbuf[2], cbuf[2];        // chunk MB records / coefficient words, one set per record bank
+    // frame downloads, slots dealt round-robin: each stream's copies go to their own DMA engine
+    hipStream_t dl[kMaxDl] = {};
+    int ndl = 1;
+    hipEvent_t decoded = nullptr;      // end of the last chunk's decode (on the context stream)
+    int frames = 0;                    // frames decoded in the last decode()
+    // per decode() state
+    std::vector<int> free_slots;
+    std::map<int, HostFrame*> inflight;  // decode index -> frame whose copy is in flight
+    std::vector<int> pend;               // pictures of the chunk whose copies are in flight
+    std::vector<int> held;               // copied pictures whose slot a later picture still reads
+    ~Lane() {
+        hipSetDevice(device);
+        for (hipStream_t st : dl)
+            if (st) hipStreamSynchronize(st);
+        if (ctx) mp2vg_synchronize(ctx);
+        dpool.reset();
+        if (decoded) hipEventDestroy(decoded);
+        for (hipStream_t st : dl)
+            if (st) hipStreamDestroy(st);
+        if (ctx) mp2vg_destroy(ctx);
+    }
+};
 }  // namespace
 
 struct mp2vg_decoder {
     mp2vg_config_t cfg{};
     mp2vg_render_fn fn = nullptr;
     void* user = nullptr;
-    mp2vg_ctx_t* ctx = nullptr;
     Geom g{};
-    int nslots = 0;
-    std::unique_ptr<FramePool> pool;
-    PinnedBuf mbuf[2], cbuf[2];        // chunk MB records / coefficient words, one set per record bank
-    // frame downloads, slots dealt round-robin: each stream's copies go to their own DMA engine
-    hipStream_t dl[kMaxDl] = {};
-    int ndl = 1;
-    hipEvent_t decoded = nullptr;      // end of the last chunk's decode (on the context stream)
+    std::vector<std::unique_ptr<Lane>> lanes;
+    std::unique_ptr<FramePool> hpool;  // pinned host frames, shared by every lane
     bool device_frames = false;        // MP2VG_DECODER_DEVICE_FRAMES: frames handed over in HBM
+    mp2vg_stream_headers_t hdrs{};     // of the last decode()
 };
 
 extern "C" int mp2vg_decoder_destroy(mp2vg_decoder_t* d) {
     if (!d) return MP2VG_E_INVALID;
-    for (hipStream_t st : d->dl)
-        if (st) hipStreamSynchronize(st);
-    if (d->ctx) mp2vg_synchronize(d->ctx);
-    d->pool.reset();
-    if (d->decoded) hipEventDestroy(d->decoded);
-    for (hipStream_t st : d->dl)
-        if (st) hipStreamDestroy(st);
-    if (d->ctx) mp2vg_destroy(d->ctx);
+    d->lanes.clear();  // synchronises every lane's streams before its buffers go
+    d->hpool.reset();
     delete d;
     return MP2VG_OK;
 }
 
-extern "C" int mp2vg_decoder_create(const mp2vg_config_t* cfg, mp2vg_render_fn fn, void* user,
-                                    mp2vg_decoder_t** out) {
-    if (!cfg || !fn || !out) return MP2VG_E_INVALID;
+extern "C" int mp2vg_decoder_create_multi(const mp2vg_config_t* cfg, const int32_t* devices, int32_t ndevices,
+                                          mp2vg_render_fn fn, void* user, mp2vg_decoder_t** out) {
+    if (!cfg || !fn || !out || !devices || ndevices < 1 || ndevices > 64) return MP2VG_E_INVALID;
     *out = nullptr;
     if (cfg->reserved & ~MP2VG_DECODER_DEVICE_FRAMES) {
         set_error("unknown decoder flags in mp2vg_config_t.reserved");
         return MP2VG_E_INVALID;
     }
-    mp2vg_config_t c = *cfg;
-    // chunk k decodes into its own slots while chunk k-1 is still being downloaded
-    c.pictures_pool_size = std::max(cfg->pictures_pool_size, 2 * kChunk + 4);
-    mp2vg_ctx_t* ctx = nullptr;
-    int rc = mp2vg_create(&c, &ctx);
-    if (rc != MP2VG_OK) return rc;
     auto* d = new mp2vg_decoder();
-    d->cfg = c;
+    d->cfg = *cfg;
+    // chunk k decodes into its own slots while chunk k-1 is still being downloaded
+    d->cfg.pictures_pool_size = std::max(cfg->pictures_pool_size, 2 * kChunk + 4);
     d->fn = fn;
     d->user = user;
-    d->ctx = ctx;
-    d->g.init(c.width, c.height, c.chroma_format);
-    d->nslots = c.pictures_pool_size;
-    d->device_frames = c.reserved & MP2VG_DECODER_DEVICE_FRAMES;
-    d->pool.reset(new FramePool(d->g.slot_bytes, d->device_frames));
-    ctx_set_launch_timing(ctx, false);  // no per-launch events on the drop-in's chunk path
-    d->ndl = kDlStreams;
-    bool sok = true;
-    for (int i = 0; i < d->ndl; i++) sok = sok && hipStreamCreateWithFlags(&d->dl[i], hipStreamNonBlocking) == hipSuccess;
-    if (!sok ||
-        hipEventCreateWithFlags(&d->decoded, hipEventDisableTiming) != hipSuccess) {
-        set_error("download stream / event creation failed");
-        mp2vg_decoder_destroy(d);
-        return MP2VG_E_HIP;
+    d->g.init(cfg->width, cfg->height, cfg->chroma_format);
+    d->device_frames = cfg->reserved & MP2VG_DECODER_DEVICE_FRAMES;
+    // frames in flight per lane: one chunk being copied, one being rendered, anchors held for display
+    const int frames_per_lane = 2 * kChunk + 4;
+    const size_t chunk_mbs = (size_t)kChunk * (cfg->width / 16) * (cfg->height / 16);
+    for (int i = 0; i < ndevices; i++) {
+        d->lanes.emplace_back(new Lane());
+        Lane& L = *d->lanes.back();
+        L.device = devices[i];
+        mp2vg_config_t c = d->cfg;
+        c.device = devices[i];
+        c.reserved = 0;
+        int rc = mp2vg_create(&c, &L.ctx);
+        if (rc != MP2VG_OK) {
+            mp2vg_decoder_destroy(d);
+            return rc;
+        }
+        L.nslots = c.pictures_pool_size;
+        ctx_set_launch_timing(L.ctx, false);  // no per-launch events on the drop-in's chunk path
+        hipSetDevice(L.device);
+        L.ndl = kDlStreams;
+        bool sok = true;
+        for (int k = 0; k < L.ndl; k++)
+            sok = sok && hipStreamCreateWithFlags(&L.dl[k], hipStreamNonBlocking) == hipSuccess;
+        if (!sok || hipEventCreateWithFlags(&L.decoded, hipEventDisableTiming) != hipSuccess) {
+            set_error("download stream / event creation failed");
+            mp2vg_decoder_destroy(d);
+            return MP2VG_E_HIP;
+        }
+        // chunk record buffers sized up front: every MB record of a chunk, and 32 coefficient
+        // words per MB (the bench stream needs 12.5; a chunk that needs more grows its set once)
+        bool ok = true;
+        for (int k = 0; k < 2; k++)
+            ok = ok && L.mbuf[k].reserve(chunk_mbs * sizeof(mp2vg_mb_t)) && L.cbuf[k].reserve(chunk_mbs * 32 * 4);
+        if (d->device_frames) {
+            L.dpool.reset(new FramePool(d->g.slot_bytes, true, L.device));
+            ok = ok && L.dpool->reserve(frames_per_lane);
+        }
+        if (!ok) {
+            set_error("pinned record buffer / device frame allocation failed");
+            mp2vg_decoder_destroy(d);
+            return MP2VG_E_NOMEM;
+        }
     }
-    // chunk record buffers sized up front: every MB record of a chunk, and 32 coefficient words
-    // per MB (the bench stream needs 12.5; a chunk that needs more grows its set once)
-    const size_t chunk_mbs = (size_t)kChunk * (c.width / 16) * (c.height / 16);
-    bool ok = true;
-    for (int i = 0; i < 2; i++)
-        ok = ok && d->mbuf[i].reserve(chunk_mbs * sizeof(mp2vg_mb_t)) && d->cbuf[i].reserve(chunk_mbs * 32 * 4);
-    // frames in flight: one chunk being copied, one being rendered, anchors held for display
-    if (!ok || !d->pool->reserve(2 * kChunk + 4)) {
-        set_error("pinned host frame allocation failed");
-        mp2vg_decoder_destroy(d);
-        return MP2VG_E_NOMEM;
+    if (!d->device_frames) {
+        d->hpool.reset(new FramePool(d->g.slot_bytes, false, devices[0]));
+        if (!d->hpool->reserve(frames_per_lane * ndevices)) {
+            set_error("pinned host frame allocation failed");
+            mp2vg_decoder_destroy(d);
+            return MP2VG_E_NOMEM;
+        }
     }
     *out = d;
     return MP2VG_OK;
+}
+
+extern "C" int mp2vg_decoder_create(const mp2vg_config_t* cfg, mp2vg_render_fn fn, void* user,
+                                    mp2vg_decoder_t** out) {
+    if (!cfg) return MP2VG_E_INVALID;
+    const int32_t dev = cfg->device;
+    return mp2vg_decoder_create_multi(cfg, &dev, 1, fn, user, out);
+}
+
+extern "C" int mp2vg_decoder_stream_headers(const mp2vg_decoder_t* d, mp2vg_stream_headers_t* out) {
+    if (!d || !out) return MP2VG_E_INVALID;
+    *out = d->hdrs;
+    return MP2VG_OK;
+}
+
+extern "C" int mp2vg_decoder_lane_frames(const mp2vg_decoder_t* d, int32_t* frames, int32_t n) {
+    if (!d) return MP2VG_E_INVALID;
+    for (int i = 0; i < n && i < (int)d->lanes.size(); i++) frames[i] = d->lanes[i]->frames;
+    return (int)d->lanes.size();
+}
+
+extern "C" int mp2vg_decoder_frames_allocated(const mp2vg_decoder_t* d) {
+    if (!d) return MP2VG_E_INVALID;
+    size_t n = d->hpool ? d->hpool->size() : 0;
+    for (auto& L : d->lanes)
+        if (L->dpool) n += L->dpool->size();
+    return (int)n;
 }
 
 extern "C" int mp2vg_decoder_decode(mp2vg_decoder_t* d, const uint8_t* buf, uint64_t len) {
@@ -226,14 +323,21 @@ extern "C" int mp2vg_decoder_decode(mp2vg_decoder_t* d, const uint8_t* buf, uint
     t0 = trace_phase("dropin: headers", t0);
     if (rc != MP2VG_OK) return rc;
     std::unique_ptr<ParseSession, void (*)(ParseSession*)> guard(ps, parse_session_free);
+    d->hdrs = *parse_session_headers(ps);
     const int32_t npics = parse_session_npics(ps);
     const mp2vg_picture_t* pics = parse_session_pictures(ps);
     std::vector<int32_t> display(parse_session_display(ps), parse_session_display(ps) + npics);
+    const int32_t* shard = parse_session_shards(ps);
+    const int nl = (int)d->lanes.size();
+    auto lane_of = [&](int p) -> Lane& { return *d->lanes[shard[p] % nl]; };
 
-    // last decode index that predicts from each picture
+    // a reference on another lane: the forward anchor of a closed GOP's leading B picture, which
+    // its macroblocks never read (mp2vg_parsed_shards); checked on its records below
+    auto foreign = [&](int q, int r) { return r >= 0 && &lane_of(r) != &lane_of(q); };
+    // last decode index that predicts from each picture (on the picture's own lane)
     std::vector<int> last_use(npics, -1);
     for (int q = 0; q < npics; q++) {
-        if (pics[q].fwd_slot >= 0) last_use[pics[q].fwd_slot] = q;
+        if (pics[q].fwd_slot >= 0 && !foreign(q, pics[q].fwd_slot)) last_use[pics[q].fwd_slot] = q;
         if (pics[q].bwd_slot >= 0) last_use[pics[q].bwd_slot] = q;
     }
 
@@ -241,8 +345,8 @@ extern "C" int mp2vg_decoder_decode(mp2vg_decoder_t* d, const uint8_t* buf, uint
     std::mutex mu;
     std::condition_variable cv;
     std::deque<HostFrame*> q;
+    std::atomic<int> held{0};  // frames queued for or inside the render callback
     bool done = false;
-    FramePool& pool = *d->pool;
     std::thread render([&]() {
         for (;;) {
             HostFrame* f;
@@ -254,14 +358,24 @@ extern "C" int mp2vg_decoder_decode(mp2vg_decoder_t* d, const uint8_t* buf, uint
                 q.pop_front();
             }
             d->fn(d->user, &f->f);
-            pool.put(f);
+            f->owner->put(f);
+            held--;
         }
     });
+    auto renderer_holds = [&]() { return held.load(); };
 
     std::vector<int> slot_of(npics, -1);
-    std::vector<int> free_slots;
-    for (int s = d->nslots - 1; s >= 0; s--) free_slots.push_back(s);
-    std::map<int, HostFrame*> ready;  // decode index -> downloaded frame
+    std::vector<uint8_t> queued(npics, 0);  // the picture's decode has been queued
+    for (auto& Lp : d->lanes) {
+        Lane& L = *Lp;
+        L.free_slots.clear();
+        for (int s = L.nslots - 1; s >= 0; s--) L.free_slots.push_back(s);
+        L.inflight.clear();
+        L.pend.clear();
+        L.held.clear();
+        L.frames = 0;
+    }
+    std::map<int, HostFrame*> ready;  // decode index -> downloaded frame, waiting for display order
     size_t next_display = 0;
     std::vector<mp2vg_picture_t> cp;
     std::vector<size_t> ncoef_of(kChunk);
@@ -269,45 +383,62 @@ extern "C" int mp2vg_decoder_decode(mp2vg_decoder_t* d, const uint8_t* buf, uint
     const uint64_t mbs_per_pic = (uint64_t)(d->cfg.width / 16) * (d->cfg.height / 16);
 
     auto finish = [&](int status) {
-        for (int i = 0; i < d->ndl; i++) hipStreamSynchronize(d->dl[i]);  // no copy may still target a pool frame
-        mp2vg_synchronize(d->ctx);
+        for (auto& Lp : d->lanes) {  // no copy may still target a pool frame
+            hipSetDevice(Lp->device);
+            for (int i = 0; i < Lp->ndl; i++) hipStreamSynchronize(Lp->dl[i]);
+            mp2vg_synchronize(Lp->ctx);
+        }
         {
             std::lock_guard<std::mutex> lk(mu);
             done = true;
         }
         cv.notify_all();
         render.join();
+        // frames an error left behind go back to their pools (a long-lived decoder must not grow)
+        for (auto& Lp : d->lanes) {
+            for (auto& kv : Lp->inflight) kv.second->owner->put(kv.second);
+            Lp->inflight.clear();
+            Lp->pend.clear();
+        }
+        for (auto& kv : ready) kv.second->owner->put(kv.second);
+        ready.clear();
         return status;
     };
 
-    // Chunk pipeline, nothing waits for the device except through an event:
+    // Chunk pipeline, per lane; nothing waits for a device except through an event:
     //   host:   gather chunk k's records (pinned) | upload (copy stream; waits only for the decode
     //           of chunk k-2, which read the same record bank) | queue decode k | complete k-1
     //   device: decode k-1 ... decode k (context stream) while the D2H copies of k-1 run (dl)
-    // A chunk's frames reach the renderer, and its slots return to the free list, only after its
-    // copies have completed; a released slot is rewritten only by a later chunk, whose decode is
-    // ordered after every earlier decode on the context stream.
-    std::map<int, HostFrame*> inflight;  // decode index -> frame whose copy is in flight
-    int pend_e = -1;                     // end of the chunk whose copies are in flight
-    int decoded_e = 0;                   // the decodes of pictures [0, decoded_e) are queued
-    auto complete_pending = [&]() -> int {
-        if (pend_e < 0) return MP2VG_OK;
+    // A chunk's frames reach the renderer, and its slots return to the lane's free list, only
+    // after its copies have completed; a released slot is rewritten only by a later chunk of the
+    // same lane, whose decode is ordered after every earlier one on that lane's context stream.
+    auto complete_pending = [&](Lane& L) -> int {
+        if (L.pend.empty()) return MP2VG_OK;
         tc = now_ms();
-        for (int i = 0; i < d->ndl; i++)
-            if (hipStreamSynchronize(d->dl[i]) != hipSuccess) return MP2VG_E_HIP;
+        hipSetDevice(L.device);
+        for (int i = 0; i < L.ndl; i++)
+            if (hipStreamSynchronize(L.dl[i]) != hipSuccess) return MP2VG_E_HIP;
         t_down += now_ms() - tc;
-        for (auto& kv : inflight) ready[kv.first] = kv.second;
-        inflight.clear();
-        // release slots no later picture predicts from
-        for (int p = 0; p < pend_e; p++)
-            if (slot_of[p] >= 0 && last_use[p] < decoded_e) {
-                free_slots.push_back(slot_of[p]);
+        for (auto& kv : L.inflight) ready[kv.first] = kv.second;
+        L.inflight.clear();
+        // release this lane's slots that no picture still to be queued predicts from (an anchor
+        // stays held until the decode of its last user is queued)
+        L.held.insert(L.held.end(), L.pend.begin(), L.pend.end());
+        size_t keep = 0;
+        for (int p : L.held) {
+            if (last_use[p] < 0 || queued[last_use[p]]) {
+                L.free_slots.push_back(slot_of[p]);
                 slot_of[p] = -1;
+            } else {
+                L.held[keep++] = p;
             }
-        pend_e = -1;
+        }
+        L.held.resize(keep);
+        L.pend.clear();
         // hand frames to the render thread in display order
         while (next_display < display.size() && ready.count(display[next_display])) {
             auto it = ready.find(display[next_display]);
+            held++;
             {
                 std::lock_guard<std::mutex> lk(mu);
                 q.push_back(it->second);
@@ -319,14 +450,19 @@ extern "C" int mp2vg_decoder_decode(mp2vg_decoder_t* d, const uint8_t* buf, uint
         return MP2VG_OK;
     };
 
-    for (int s = 0; s < npics; s += kChunk) {
-        int e = std::min(npics, s + kChunk);
-        // slots for this chunk (the previous chunk's copies finish first when the pool runs dry)
+    // one chunk: pictures [s, e) in decode order, all of lane L
+    auto run_chunk = [&](Lane& L, int s, int e) -> int {
+        int rc;
+        hipSetDevice(L.device);
+        // slots for this chunk (the lane's previous chunk's copies finish first when it runs dry)
         for (int p = s; p < e; p++) {
-            if (free_slots.empty() && (rc = complete_pending()) != MP2VG_OK) return finish(rc);
-            if (free_slots.empty()) return finish(MP2VG_E_STATE);
-            slot_of[p] = free_slots.back();
-            free_slots.pop_back();
+            if (L.free_slots.empty() && (rc = complete_pending(L)) != MP2VG_OK) return rc;
+            if (L.free_slots.empty()) {
+                set_error("frame slot pool exhausted (a picture references a picture outside its chunk window)");
+                return MP2VG_E_STATE;
+            }
+            slot_of[p] = L.free_slots.back();
+            L.free_slots.pop_back();
         }
         // chunk records with physical slots; MB and coefficient offsets local to the chunk,
         // gathered straight into pinned memory
@@ -334,26 +470,36 @@ extern "C" int mp2vg_decoder_decode(mp2vg_decoder_t* d, const uint8_t* buf, uint
         tc = now_ms();
         size_t nc = 0;
         for (int p = s; p < e; p++) {
-            if ((rc = parse_session_wait(ps, p)) != MP2VG_OK) return finish(rc);
+            if ((rc = parse_session_wait(ps, p)) != MP2VG_OK) return rc;
             ncoef_of[p - s] = parse_session_ncoefs(ps, p);
             nc += ncoef_of[p - s];
         }
         t_wait += now_ms() - tc;
         const size_t nm = (size_t)(e - s) * mbs_per_pic;
         tc = now_ms();
-        // this chunk's buffer set fed the upload two chunks back: its copies must have landed
-        const int hb = ctx_next_bank(d->ctx);
-        if ((rc = ctx_wait_upload(d->ctx, hb)) != MP2VG_OK) return finish(rc);
-        if (nc >= (1ull << 32) || !d->mbuf[hb].reserve(nm * sizeof(mp2vg_mb_t)) ||
-            !d->cbuf[hb].reserve(std::max<size_t>(nc, 1) * 4))
-            return finish(MP2VG_E_NOMEM);
-        auto* cm = (mp2vg_mb_t*)d->mbuf[hb].p;
-        auto* cc = (uint32_t*)d->cbuf[hb].p;
+        // this chunk's buffer set fed the lane's upload two chunks back: its copies must have landed
+        const int hb = ctx_next_bank(L.ctx);
+        if ((rc = ctx_wait_upload(L.ctx, hb)) != MP2VG_OK) return rc;
+        if (nc >= (1ull << 32) || !L.mbuf[hb].reserve(nm * sizeof(mp2vg_mb_t)) ||
+            !L.cbuf[hb].reserve(std::max<size_t>(nc, 1) * 4))
+            return MP2VG_E_NOMEM;
+        auto* cm = (mp2vg_mb_t*)L.mbuf[hb].p;
+        auto* cc = (uint32_t*)L.cbuf[hb].p;
         for (int i = 0, base = 0; i < e - s; base += (int)ncoef_of[i], i++) base_of[i] = (uint32_t)base;
         parallel_for(e - s, 8, [&](int i) {
             parse_session_append(ps, s + i, cm + (size_t)i * mbs_per_pic, cc + base_of[i], base_of[i]);
         });
-        for (auto& P : cp) {
+        for (int i = 0; i < e - s; i++) {
+            mp2vg_picture_t& P = cp[i];
+            if (foreign(s + i, P.fwd_slot)) {
+                const mp2vg_mb_t* m = cm + (size_t)i * mbs_per_pic;
+                for (uint64_t k = 0; k < mbs_per_pic; k++)
+                    if (!(m[k].flags & MP2VG_MB_INTRA) && ((m[k].flags & MP2VG_MB_FWD) || !(m[k].flags & MP2VG_MB_BWD))) {
+                        set_error("a B picture of a closed GOP predicts forward across GOPs: decode it on one device");
+                        return MP2VG_E_UNSUPPORTED;
+                    }
+                P.fwd_slot = -1;
+            }
             P.dst_slot = slot_of[P.dst_slot];
             if (P.fwd_slot >= 0) P.fwd_slot = slot_of[P.fwd_slot];
             if (P.bwd_slot >= 0) P.bwd_slot = slot_of[P.bwd_slot];
@@ -361,21 +507,24 @@ extern "C" int mp2vg_decoder_decode(mp2vg_decoder_t* d, const uint8_t* buf, uint
         }
         t_gather += now_ms() - tc;
         tc = now_ms();
-        rc = batch_upload_pinned(d->ctx, cp.data(), (int32_t)cp.size(), cm, nm, cc, nc);
+        rc = batch_upload_pinned(L.ctx, cp.data(), (int32_t)cp.size(), cm, nm, cc, nc);
         t_up += now_ms() - tc;
         tc = now_ms();
-        if (rc == MP2VG_OK) rc = mp2vg_batch_decode(d->ctx);
-        if (rc == MP2VG_OK && hipEventRecord(d->decoded, ctx_stream(d->ctx)) != hipSuccess) rc = MP2VG_E_HIP;
+        if (rc == MP2VG_OK) rc = mp2vg_batch_decode(L.ctx);
+        if (rc == MP2VG_OK && hipEventRecord(L.decoded, ctx_stream(L.ctx)) != hipSuccess) rc = MP2VG_E_HIP;
         t_dec += now_ms() - tc;
-        if (rc != MP2VG_OK) return finish(rc);
-        decoded_e = e;
-        if ((rc = complete_pending()) != MP2VG_OK) return finish(rc);
-        // copies of this chunk into frame_c-layout host frames, one DMA per slot, after its decode
-        for (int i = 0; i < d->ndl; i++)
-            if (hipStreamWaitEvent(d->dl[i], d->decoded, 0) != hipSuccess) return finish(MP2VG_E_HIP);
+        if (rc != MP2VG_OK) return rc;
+        for (int p = s; p < e; p++) queued[p] = 1;
+        L.frames += e - s;
+        if ((rc = complete_pending(L)) != MP2VG_OK) return rc;
+        // copies of this chunk into frame_c-layout frames, one DMA per slot, after its decode
+        hipSetDevice(L.device);
+        for (int i = 0; i < L.ndl; i++)
+            if (hipStreamWaitEvent(L.dl[i], L.decoded, 0) != hipSuccess) return MP2VG_E_HIP;
+        FramePool& pool = d->device_frames ? *L.dpool : *d->hpool;
         for (int p = s; p < e; p++) {
-            HostFrame* hf = pool.get();
-            if (!hf) return finish(MP2VG_E_NOMEM);
+            HostFrame* hf = pool.get(renderer_holds);
+            if (!hf) return MP2VG_E_NOMEM;
             for (int i = 0; i < 3; i++) {
                 hf->f.planes[i] = hf->data + d->g.plane_off[i];
                 hf->f.width[i] = d->g.pw[i];
@@ -384,21 +533,38 @@ extern "C" int mp2vg_decoder_decode(mp2vg_decoder_t* d, const uint8_t* buf, uint
             }
             hf->f.picture_coding_type = pics[p].picture_coding_type;
             hf->f.decode_index = p;
+            hf->f.device = L.device;
             void* src = nullptr;
-            rc = mp2vg_slot_device_ptr(d->ctx, slot_of[p], &src);
+            rc = mp2vg_slot_device_ptr(L.ctx, slot_of[p], &src);
+            hipSetDevice(L.device);
             if (rc == MP2VG_OK && hipMemcpyAsync(hf->data, src, d->g.slot_bytes,
                                                  d->device_frames ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost,
-                                                 d->dl[p % d->ndl]) != hipSuccess)
+                                                 L.dl[p % L.ndl]) != hipSuccess)
                 rc = MP2VG_E_HIP;
             if (rc != MP2VG_OK) {
-                pool.put(hf);
-                return finish(rc);
+                hf->owner->put(hf);
+                return rc;
             }
-            inflight[p] = hf;
+            L.inflight[p] = hf;
         }
-        pend_e = e;
+        L.pend.clear();
+        for (int p = s; p < e; p++) L.pend.push_back(p);
+        return MP2VG_OK;
+    };
+
+    // chunks: up to kChunk consecutive pictures of one lane; with several lanes a chunk also ends
+    // where the stream moves to the next shard's lane, so the chunks (and the parse window) still
+    // advance in decode order and every lane decodes while the next one is being fed
+    for (int s = 0; s < npics;) {
+        Lane& L = lane_of(s);
+        int e = s + 1;
+        while (e < npics && e - s < kChunk && (nl == 1 || &lane_of(e) == &L)) e++;
+        if ((rc = run_chunk(L, s, e)) != MP2VG_OK) return finish(rc);
+        s = e;
     }
-    if ((rc = complete_pending()) != MP2VG_OK) return finish(rc);
+    for (auto& Lp : d->lanes)
+        if ((rc = complete_pending(*Lp)) != MP2VG_OK) return finish(rc);
+    if (next_display != display.size()) set_error("frames left undelivered in display order");
     rc = finish(next_display == display.size() ? MP2VG_OK : MP2VG_E_STATE);
     trace_phase("dropin: parse wait (sum)", now_ms() - t_wait);
     trace_phase("dropin: gather (sum)", now_ms() - t_gather);

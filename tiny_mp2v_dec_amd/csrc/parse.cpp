@@ -57,6 +57,9 @@ struct PicWork {
     PictureHdr hdr;
     int fwd = -1, bwd = -1;   // decode indices of reference pictures (L0 / L1)
     int gop = -1;
+    // a B picture between the first two anchors of a GOP with closed_gop = 1: it predicts only
+    // backward (ISO 13818-2 6.3.8), so its forward reference is not a dependency for sharding
+    bool closed_leading_b = false;
     uint8_t W[4][64] = {};
     std::vector<SliceJob> slices;
 };
@@ -98,6 +101,7 @@ struct Ctx {
     int width, height, mbw, mbh;
     int vertical_size_value = 0;
     std::vector<PicWork> pics;
+    mp2vg_stream_headers_t hdrs{};
 };
 
 #define FAIL(code, msg)          \
@@ -409,6 +413,9 @@ struct ParsedImpl {
     std::vector<uint32_t, NoInitAlloc<uint32_t>> coefs;
     std::vector<int32_t> display;
     std::vector<int32_t> gop;
+    std::vector<int32_t> shard;  // independent decode-order runs (mp2vg_parsed_shards)
+    int32_t nshards = 0;
+    mp2vg_stream_headers_t hdrs{};
 };
 
 }  // namespace mp2vg
@@ -558,20 +565,64 @@ int parse_session_start(const uint8_t* buf, uint64_t len, const mp2vg_config_t* 
     int gop = -1;
     int ref_frames[2] = {-1, -1};
     bool seq_end = false;
+    bool gop_closed = false;
+    int gop_anchors = 0;  // anchors decoded since the last group_of_pictures_header
     for (size_t k = 0; k < sc.size() && !seq_end; k++) {
         uint64_t off = sc[k];
         uint64_t end = (k + 1 < sc.size()) ? sc[k + 1] : len;
         uint8_t code = buf[off + 3];
         BitReader br(buf + off, buf + end);
         br.skip(32);
-        if (code == 0xB3) {  // sequence_header (mp2v_hdr.cpp:4-21)
-            br.skip(12);
-            C.vertical_size_value = (int)br.read(12);
+        if (code == 0xB3) {  // sequence_header (mp2v_hdr.cpp:4-21): a later one overwrites
+            mp2vg_sequence_header_t& sh = C.hdrs.sequence_header;
+            sh.sequence_header_code = 0x1B3;
+            sh.horizontal_size_value = br.read(12);
+            sh.vertical_size_value = br.read(12);
+            sh.aspect_ratio_information = br.read(4);
+            sh.frame_rate_code = br.read(4);
+            sh.bit_rate_value = br.read(18);
+            br.skip(1);  // marker_bit
+            sh.vbv_buffer_size_value = br.read(10);
+            sh.constrained_parameters_flag = br.read(1);
+            sh.load_intra_quantiser_matrix = br.read(1);
+            if (sh.load_intra_quantiser_matrix)
+                for (int i = 0; i < 64; i++) sh.intra_quantiser_matrix[i] = (uint8_t)br.read(8);
+            sh.load_non_intra_quantiser_matrix = br.read(1);
+            if (sh.load_non_intra_quantiser_matrix)
+                for (int i = 0; i < 64; i++) sh.non_intra_quantiser_matrix[i] = (uint8_t)br.read(8);
+            C.vertical_size_value = (int)sh.vertical_size_value;
         } else if (code == 0xB5) {  // extension (decoder.cpp:202-242)
             int id = (int)br.read(4);
             if (id == 1) {  // sequence_extension (mp2v_hdr.cpp:23-37)
-                br.skip(8 + 1);
-                seq_chroma = (int)br.read(2);
+                mp2vg_sequence_extension_t& se = C.hdrs.sequence_extension;
+                se.extension_start_code_identifier = (uint32_t)id;
+                se.profile_and_level_indication = br.read(8);
+                se.progressive_sequence = br.read(1);
+                se.chroma_format = br.read(2);
+                se.horizontal_size_extension = br.read(2);
+                se.vertical_size_extension = br.read(2);
+                se.bit_rate_extension = br.read(12);
+                br.skip(1);  // marker_bit
+                se.vbv_buffer_size_extension = br.read(8);
+                se.low_delay = br.read(1);
+                se.frame_rate_extension_n = br.read(2);
+                se.frame_rate_extension_d = br.read(5);
+                seq_chroma = (int)se.chroma_format;
+            } else if (id == 2) {  // sequence_display_extension (mp2v_hdr.cpp:39-52)
+                mp2vg_sequence_display_extension_t& de = C.hdrs.sequence_display_extension;
+                de = mp2vg_sequence_display_extension_t{};
+                de.extension_start_code_identifier = (uint32_t)id;
+                de.video_format = br.read(3);
+                de.colour_description = br.read(1);
+                if (de.colour_description) {
+                    de.colour_primaries = br.read(8);
+                    de.transfer_characteristics = br.read(8);
+                    de.matrix_coefficients = br.read(8);
+                }
+                de.display_horizontal_size = br.read(14);
+                br.skip(1);  // marker_bit
+                de.display_vertical_size = br.read(14);
+                C.hdrs.have_sequence_display_extension = 1;
             } else if (id == 5) {
                 set_error("scalable extensions are not supported by the reference path");
                 return MP2VG_E_UNSUPPORTED;
@@ -597,8 +648,16 @@ int parse_session_start(const uint8_t* buf, uint64_t len, const mp2vg_config_t* 
                         for (int i = 0; i < 64; i++) h.qme[m][i] = (uint8_t)br.read(8);
                 }
             }
-        } else if (code == 0xB8) {  // group_of_pictures_header
+        } else if (code == 0xB8) {  // group_of_pictures_header (mp2v_hdr.cpp:77-83)
             gop++;
+            mp2vg_group_of_pictures_header_t& gh = C.hdrs.group_of_pictures_header;
+            gh.group_start_code = 0x1B8;
+            gh.time_code = br.read(25);
+            gh.closed_gop = br.read(1);
+            gh.broken_link = br.read(1);
+            C.hdrs.have_group_of_pictures_header = 1;
+            gop_closed = gh.closed_gop != 0;
+            gop_anchors = 0;
         } else if (code == 0x00) {  // picture_start_code (decoder.cpp:294-305)
             PicWork pw;
             pw.hdr.temporal_reference = (int)br.read(10);
@@ -613,9 +672,11 @@ int parse_session_start(const uint8_t* buf, uint64_t len, const mp2vg_config_t* 
                 pw.fwd = ref_frames[1];  // I/P: dependency on the newest anchor (L0)
                 ref_frames[0] = ref_frames[1];
                 ref_frames[1] = idx;
+                gop_anchors++;
             } else {
                 pw.fwd = ref_frames[0];
                 pw.bwd = ref_frames[1];
+                pw.closed_leading_b = gop_closed && gop_anchors == 1;
             }
             if (pw.hdr.pct == 1) pw.fwd = -1;  // I pictures never predict
             C.pics.push_back(pw);
@@ -648,6 +709,16 @@ int parse_session_start(const uint8_t* buf, uint64_t len, const mp2vg_config_t* 
             return MP2VG_E_UNSUPPORTED;
         }
         if (h.pct == 2 && P.fwd < 0) { set_error("P picture without a reference"); return MP2VG_E_UNSUPPORTED; }
+        // f_code of every direction the picture may code vectors for is 1..9 (0 is forbidden and
+        // the reference would read f_code - 1 = -1 residual bits, mb_decoder.cpp:500-505)
+        for (int s = 0; s < 2; s++) {
+            const bool used = (s == 0 && (h.pct != 1 || h.concealment_motion_vectors)) || (s == 1 && h.pct == 3);
+            for (int t = 0; t < 2 && used; t++)
+                if (h.f_code[s][t] < 1 || h.f_code[s][t] > 9) {
+                    set_error("f_code outside 1..9 for a direction the picture codes vectors for");
+                    return MP2VG_E_UNSUPPORTED;
+                }
+        }
         if (P.slices.empty()) { set_error("picture without slices"); return MP2VG_E_BITSTREAM; }
         build_W(h.qme, h.alternate_scan, P.W);
     }
@@ -695,6 +766,26 @@ int parse_session_start(const uint8_t* buf, uint64_t len, const mp2vg_config_t* 
         memcpy(d.W, P.W, sizeof d.W);
         res->gop.push_back(P.gop);
     }
+    res->hdrs = C.hdrs;
+    // ---- independent shards: a new one starts at p when no picture from p on predicts from a
+    // picture before p (references are the two latest anchors, decoder.cpp:299-304) ----
+    {
+        res->shard.assign(npics, 0);
+        int32_t lo = npics;  // min reference of pictures >= p
+        std::vector<uint8_t> starts(npics, 0);
+        for (int p = npics - 1; p >= 0; p--) {
+            const PicWork& P = C.pics[p];
+            if (P.fwd >= 0 && !P.closed_leading_b) lo = std::min(lo, (int32_t)P.fwd);
+            if (P.hdr.pct == 3 && P.bwd >= 0) lo = std::min(lo, (int32_t)P.bwd);
+            starts[p] = lo >= p;
+        }
+        int32_t sh = -1;
+        for (int p = 0; p < npics; p++) {
+            if (starts[p] || sh < 0) sh++;
+            res->shard[p] = sh;
+        }
+        res->nshards = sh + 1;
+    }
     // ---- display order: the reference's output scheduler (decoder.cpp:346-369) ----
     {
         int held = -1;
@@ -719,6 +810,8 @@ int parse_session_start(const uint8_t* buf, uint64_t len, const mp2vg_config_t* 
 int parse_session_npics(const ParseSession* s) { return (int)s->C.pics.size(); }
 const mp2vg_picture_t* parse_session_pictures(const ParseSession* s) { return s->res->pics.data(); }
 const int32_t* parse_session_display(const ParseSession* s) { return s->res->display.data(); }
+const int32_t* parse_session_shards(const ParseSession* s) { return s->res->shard.data(); }
+const mp2vg_stream_headers_t* parse_session_headers(const ParseSession* s) { return &s->res->hdrs; }
 int parse_session_wait(ParseSession* s, int p) { return s->wait(p); }
 void parse_session_free(ParseSession* s) { delete s; }
 
@@ -826,12 +919,22 @@ extern "C" const mp2vg_mb_t* mp2vg_parsed_mbs(const mp2vg_parsed_t* p) { return 
 extern "C" const uint32_t* mp2vg_parsed_coefs(const mp2vg_parsed_t* p) { return p ? p->coefs.data() : nullptr; }
 extern "C" int mp2vg_parsed_display_order(const mp2vg_parsed_t* p, int32_t* order, int32_t n) {
     if (!p || !order || n < (int32_t)p->display.size()) return MP2VG_E_INVALID;
-    memcpy(order, p->display.data(), p->display.size() * 4);
+    if (!p->display.empty()) memcpy(order, p->display.data(), p->display.size() * 4);
     return (int)p->display.size();
 }
 extern "C" int mp2vg_parsed_gop_index(const mp2vg_parsed_t* p, int32_t* gop, int32_t n) {
     if (!p || !gop || n < (int32_t)p->gop.size()) return MP2VG_E_INVALID;
-    memcpy(gop, p->gop.data(), p->gop.size() * 4);
+    if (!p->gop.empty()) memcpy(gop, p->gop.data(), p->gop.size() * 4);
     return (int)p->gop.size();
+}
+extern "C" int mp2vg_parsed_stream_headers(const mp2vg_parsed_t* p, mp2vg_stream_headers_t* out) {
+    if (!p || !out) return MP2VG_E_INVALID;
+    *out = p->hdrs;
+    return MP2VG_OK;
+}
+extern "C" int mp2vg_parsed_shards(const mp2vg_parsed_t* p, int32_t* shard, int32_t n) {
+    if (!p || !shard || n < (int32_t)p->shard.size()) return MP2VG_E_INVALID;
+    if (!p->shard.empty()) memcpy(shard, p->shard.data(), p->shard.size() * 4);
+    return p->nshards;
 }
 extern "C" void mp2vg_parsed_free(mp2vg_parsed_t* p) { delete p; }

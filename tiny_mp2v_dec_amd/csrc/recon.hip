@@ -510,6 +510,9 @@ __device__ __forceinline__ void store_pass(uint32_t r0, uint32_t r1, bool live, 
     uint8_t* dst = dst_slot + gsel(geo.plane_off, plane) +
                    mul24_asm((r0 >> 16) * phm + py, (uint32_t)gsel(geo.stride, plane)) + (int)(r0 & 0xffff) * pw;
     dst = live ? dst : wsink;  // branch-free: every lane stores (see Tap)
+    if (ABL & 8192)  // dev ablation (timing only): each store instruction writes 1 KB contiguous
+        dst = dst_slot + ((((r0 & 0xffff) + (r0 >> 16) * 128u) * 3u + (uint32_t)J) * 1024u + (uint32_t)lane * 16u) %
+                             (uint32_t)(geo.plane_off[1] - 1024);
     if (ABL & 8) {
         asm volatile("" ::"v"(out[0]), "v"(out[1]), "v"(out[2]), "v"(out[3]), "v"(dst));
     } else if (ABL & 4096) {  // dev ablation (timing only): one dword per row store (1/4, 1/2 bytes)
@@ -968,6 +971,7 @@ hipError_t launch_recon(int cf, int mcm, const KArgs& a, hipStream_t stream) {
         case 2056: return launch_mcm<1, 2056>(mcm, a, g, stream);
         case 3072: return launch_mcm<1, 3072>(mcm, a, g, stream);
         case 4096: return launch_mcm<1, 4096>(mcm, a, g, stream);
+        case 8192: return launch_mcm<1, 8192>(mcm, a, g, stream);
         default: return hipErrorInvalidValue;
         }
     }

@@ -312,6 +312,8 @@ int parse_session_start(const uint8_t* buf, uint64_t len, const mp2vg_config_t* 
 int parse_session_npics(const ParseSession* s);
 const mp2vg_picture_t* parse_session_pictures(const ParseSession* s);  // dst_slot = decode index
 const int32_t* parse_session_display(const ParseSession* s);           // npics entries
+const int32_t* parse_session_shards(const ParseSession* s);            // npics entries (mp2vg_parsed_shards)
+const mp2vg_stream_headers_t* parse_session_headers(const ParseSession* s);
 int parse_session_wait(ParseSession* s, int p);  // status of picture p once its slices are parsed
 size_t parse_session_ncoefs(const ParseSession* s, int p);  // after parse_session_wait
 void parse_session_append(ParseSession* s, int p, mp2vg_mb_t* mbs_out, uint32_t* coefs_out, uint32_t base);

@@ -10,6 +10,12 @@ the HIP kernels on the GPU, and each frame is copied into a host frame with the 
 frame_c layout before the renderer runs.  A frame is valid only during the callback (reference
 frame pool recycling, threads.cpp:75-80); copy it to keep it.
 
+decoder_config_t(devices=[0, 1, ...]) shards the stream by GOP over several GPUs
+(mp2vg_decoder_create_multi: independent shard s -> devices[s % len(devices)]); frames still reach
+the renderer in display order.  After decode(), m_sequence_header / m_sequence_extension /
+m_sequence_display_extension / m_group_of_pictures_header hold the stream's headers as the
+reference's public members do (decoder.h:124-130).
+
 decoder_config_t(device_frames=True) opts into the device-pointer output path
 (MP2VG_DECODER_DEVICE_FRAMES): frames stay in HBM (no PCIe download), frame_c.device_ptr(i) gives
 the plane's device address and get_planes(i) copies the plane to the host on demand.
@@ -33,6 +39,7 @@ class decoder_config_t:  # noqa: N801  (reference name)
     reordering: bool = True
     device: int = 0
     device_frames: bool = False
+    devices: list = None  # GOP sharding over these devices (None: [device])
 
 
 MP2VG_DECODER_DEVICE_FRAMES = 1  # include/mp2vg.h
@@ -62,6 +69,7 @@ class frame_c:  # noqa: N801  (reference name)
         self.is_device = device
         self.picture_coding_type = f.picture_coding_type
         self.decode_index = f.decode_index
+        self.device = f.device
 
     def get_planes(self, i):
         """numpy view of plane i: height x stride bytes (only valid during the callback)."""
@@ -112,8 +120,17 @@ class mp2v_decoder_c:  # noqa: N801  (reference name)
 
         self._cb = _lib.RENDER_FN(_cb)  # keep the trampoline alive
         self._h = ctypes.c_void_p()
-        check(lib().mp2vg_decoder_create(ctypes.byref(self._cfg), self._cb, None, ctypes.byref(self._h)),
-              "decoder_create")
+        devs = list(config.devices) if config.devices else [config.device]
+        self._devices = devs
+        arr = (ctypes.c_int32 * len(devs))(*devs)
+        check(lib().mp2vg_decoder_create_multi(ctypes.byref(self._cfg), arr, len(devs), self._cb, None,
+                                               ctypes.byref(self._h)), "decoder_create")
+        self.user_data = []
+        self.m_sequence_header = None
+        self.m_sequence_extension = None
+        self.m_sequence_display_extension = None
+        self.m_sequence_scalable_extension = None  # scalable streams are rejected
+        self.m_group_of_pictures_header = None
 
     def decode(self, buffer, length=None):
         data = bytes(buffer) if not isinstance(buffer, (bytes, bytearray)) else buffer
@@ -123,10 +140,32 @@ class mp2v_decoder_c:  # noqa: N801  (reference name)
         # no copy: the parser reads exactly [0, n) (zeros past the end, syntax.h BitReader)
         buf = np.frombuffer(data, dtype=np.uint8, count=n)
         check(lib().mp2vg_decoder_decode(self._h, buf.ctypes.data_as(ctypes.c_void_p), n), "decoder_decode")
+        h = _lib.StreamHeaders()
+        check(lib().mp2vg_decoder_stream_headers(self._h, ctypes.byref(h)), "decoder_stream_headers")
+        self.m_sequence_header = h.sequence_header
+        self.m_sequence_extension = h.sequence_extension
+        self.m_sequence_display_extension = h.sequence_display_extension if h.have_sequence_display_extension else None
+        self.m_group_of_pictures_header = h.group_of_pictures_header if h.have_group_of_pictures_header else None
         if self._error is not None:
             e, self._error = self._error, None
             raise e
         return True
+
+    def flush(self, cur_pic=None):
+        """reference decoder.h:100; decode() already submits and drains everything."""
+        return None
+
+    def lane_frames(self):
+        """Frames each device lane decoded in the last decode() (lane i = devices[i])."""
+        n = len(self._devices)
+        out = (ctypes.c_int32 * n)()
+        lib().mp2vg_decoder_lane_frames(self._h, out, n)
+        return list(out)
+
+    def frames_allocated(self):
+        """Frame buffers held by the decoder's frame pools (bounded: the renderer back-pressures
+        the decoder as the reference's fixed picture pool does)."""
+        return lib().mp2vg_decoder_frames_allocated(self._h)
 
     def close(self):
         if self._h:

@@ -40,6 +40,13 @@ def generate_es(**kw):
         lib().mp2vg_free(ptr)
 
 
+def check_count(status, what):
+    """An entry point that returns a count (>= 0) or an MP2VG_E_* status."""
+    if status < 0:
+        check(status, what)
+    return status
+
+
 class Parsed:
     """Records of a whole elementary stream (pictures in decode order; slot = decode index)."""
 
@@ -63,6 +70,11 @@ class Parsed:
             gop = (ctypes.c_int32 * max(n, 1))()
             lib().mp2vg_parsed_gop_index(h, gop, n)
             self.gop = np.array(gop[:n], dtype=np.int32)
+            shard = (ctypes.c_int32 * max(n, 1))()
+            self.nshards = check_count(lib().mp2vg_parsed_shards(h, shard, n), "parsed_shards")
+            self.shard = np.array(shard[:n], dtype=np.int32)
+            self.headers = _lib.StreamHeaders()
+            check(lib().mp2vg_parsed_stream_headers(h, ctypes.byref(self.headers)), "parsed_stream_headers")
         finally:
             lib().mp2vg_parsed_free(h)
 
