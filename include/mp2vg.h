@@ -174,6 +174,10 @@ int  mp2vg_last_batch_time(mp2vg_ctx_t* ctx, float* ms);
  * per-launch device times (launch_ms[0..min(count, max)), may be NULL); synchronises */
 int  mp2vg_batch_times(mp2vg_ctx_t* ctx, int32_t back, float* batch_ms, float* launch_ms, int32_t max,
                        int32_t* count);
+/* device time (ms) from the start of the batch decoded `back_first` decodes ago to the end of the
+ * one `back_last` decodes ago (back_first >= back_last; the last 64 are kept): the device span of
+ * back-to-back batches, whose picture sets overlap across batch boundaries; synchronises */
+int  mp2vg_batches_span(mp2vg_ctx_t* ctx, int32_t back_first, int32_t back_last, float* ms);
 /* copy one frame slot to host planes (each plane written width x height, tightly packed if
  * dst_stride is 0); synchronous */
 int  mp2vg_download_slot(mp2vg_ctx_t* ctx, int32_t slot, uint8_t* dst_planes[3],

@@ -64,6 +64,7 @@ struct Bank {
     SliceDesc* d_slices = nullptr;
     size_t cap_slices = 0;
     std::vector<Launch> launches;  // slice ranges per (dependency level, picture type)
+    std::vector<std::vector<int32_t>> foot;  // per picture set: the slots it writes or reads
     int32_t npics = 0;
     hipEvent_t uploaded = nullptr;  // on ustream, after the bank's copies
     hipEvent_t consumed = nullptr;  // on stream, after the last decode that read the bank
@@ -73,10 +74,11 @@ struct Bank {
 struct mp2vg_ctx {
     mp2vg_config_t cfg{};
     Geom g{};
-    hipStream_t stream = nullptr;  // set 0's stream; every API call synchronises on it
+    hipStream_t stream = nullptr;  // joins every set of each batch; every API call synchronises on it
     hipStream_t ustream = nullptr;  // record uploads
-    std::vector<hipStream_t> sstreams;  // sets 1.. (created on first use)
-    std::vector<hipEvent_t> sev;        // end of each set's launches
+    std::vector<hipStream_t> sstreams;  // one per picture set (created on first use)
+    std::vector<hipEvent_t> sev;        // end of each set's launches in the last batch
+    std::vector<std::vector<uint8_t>> last_foot;  // slots each set of the last batch touched
     uint8_t* d_pool = nullptr;
     int32_t nslots = 0;
     int nstreams = 2;  // independent picture sets per batch (default_streams)
@@ -204,6 +206,7 @@ extern "C" int mp2vg_destroy(mp2vg_ctx_t* c) {
     hipFree(c->d_dslots);
     hipFree(c->d_digest);
     if (c->h_stage) hipHostFree(c->h_stage);
+    for (auto st : c->sstreams) hipStreamSynchronize(st);
     for (auto e : c->sev) hipEventDestroy(e);
     for (auto st : c->sstreams) hipStreamDestroy(st);
     if (c->ustream) hipStreamDestroy(c->ustream);
@@ -230,13 +233,14 @@ extern "C" int mp2vg_reserve_slots(mp2vg_ctx_t* c, int32_t nslots) {
     HIPCHK(hipStreamSynchronize(c->stream));
     c->d_pool = p;
     c->nslots = nslots;
+    c->last_foot.clear();  // every set of every batch is done (c->stream joined them)
     return MP2VG_OK;
 }
 
 // Validate the batch so no kernel access can leave its buffers, and compute dependency levels.
 static int plan_batch(mp2vg_ctx_t* c, const mp2vg_picture_t* pics, int32_t npics, const mp2vg_mb_t* mbs,
                       uint64_t nmbs, const uint32_t* coefs, uint64_t ncoefs, std::vector<SliceDesc>& slices,
-                      std::vector<Launch>& launches) {
+                      std::vector<Launch>& launches, std::vector<std::vector<int32_t>>* foot = nullptr) {
     const int mbw = c->cfg.width / 16, mbh = c->cfg.height / 16;
     const int nb = c->g.nblocks;
     std::vector<int> level(npics, 0);
@@ -353,6 +357,20 @@ static int plan_batch(mp2vg_ctx_t* c, const mp2vg_picture_t* pics, int32_t npics
         set_of[p] = root_set[r];
         load[set_of[p]]++;
     }
+    if (foot) {  // each set's slot footprint: the next batch's sets wait only for overlapping ones
+        foot->assign(nsets, {});
+        std::vector<int8_t> seen((size_t)c->nslots * nsets, 0);
+        for (int p = 0; p < npics; p++) {
+            const mp2vg_picture_t& P = pics[p];
+            const int sl[3] = {P.dst_slot, uses_of[2 * (size_t)p] ? P.fwd_slot : -1,
+                               uses_of[2 * (size_t)p + 1] ? P.bwd_slot : -1};
+            for (int x : sl)
+                if (x >= 0 && !seen[(size_t)set_of[p] * c->nslots + x]) {
+                    seen[(size_t)set_of[p] * c->nslots + x] = 1;
+                    (*foot)[set_of[p]].push_back(x);
+                }
+        }
+    }
     slices.clear();
     launches.clear();
     for (int set = 0; set < nsets; set++)
@@ -404,8 +422,9 @@ static int batch_upload(mp2vg_ctx_t* c, const mp2vg_picture_t* pics, int32_t npi
     c->batch_ready = false;
     std::vector<SliceDesc> slices;
     std::vector<Launch> lb;
+    std::vector<std::vector<int32_t>> foot;
     double tp = now_ms();
-    int rc = plan_batch(c, pics, npics, mbs, nmbs, coefs, ncoefs, slices, lb);
+    int rc = plan_batch(c, pics, npics, mbs, nmbs, coefs, ncoefs, slices, lb, &foot);
     if (rc != MP2VG_OK) return rc;
     tp = trace_phase("upload: plan", tp);
     // the other bank from the last upload; the decode queued on it is still allowed to run
@@ -430,6 +449,7 @@ static int batch_upload(mp2vg_ctx_t* c, const mp2vg_picture_t* pics, int32_t npi
     if (!async) HIPCHK(hipStreamSynchronize(c->ustream));
     trace_phase("upload: copy", tp);
     b.launches = std::move(lb);
+    b.foot = std::move(foot);
     b.npics = npics;
     c->cur = k;
     c->batch_ready = true;
@@ -516,12 +536,15 @@ extern "C" int mp2vg_batch_decode(mp2vg_ctx_t* c) {
         a.stride[i] = c->g.stride[i];
         a.ph[i] = c->g.ph[i];
     }
-    // Each picture set's level launches run back to back on its own stream; the set streams
-    // start after everything queued before this batch (evb[0]) and set 0's stream waits for all
-    // of them at the end, so API calls that synchronise on c->stream see the whole batch.
+    // Each picture set's level launches run back to back on its own stream.  A set starts once
+    // its records have landed and the sets of the previous batch that touched any of its slots
+    // (as destination or used reference) are done -- not after the whole previous batch, so
+    // back-to-back batches overlap set by set and one set's launch tails fill with the other's
+    // work across batch boundaries too.  c->stream joins every set at the end, so API calls that
+    // synchronise on it see the whole batch (they all do before touching slots).
     int nsets = 1;
     for (const Launch& L : launches) nsets = std::max(nsets, L.set + 1);
-    while ((int)c->sstreams.size() < nsets - 1) {
+    while ((int)c->sstreams.size() < nsets) {
         hipStream_t st;
         hipEvent_t e;
         HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
@@ -529,10 +552,17 @@ extern "C" int mp2vg_batch_decode(mp2vg_ctx_t* c) {
         c->sstreams.push_back(st);
         c->sev.push_back(e);
     }
-    auto stream_of = [&](int set) { return set == 0 ? c->stream : c->sstreams[set - 1]; };
-    HIPCHK(hipStreamWaitEvent(c->stream, b.uploaded, 0));
-    HIPCHK(hipEventRecord(H.b[0], c->stream));
-    for (int set = 1; set < nsets; set++) HIPCHK(hipStreamWaitEvent(stream_of(set), H.b[0], 0));
+    auto stream_of = [&](int set) { return c->sstreams[set]; };
+    for (int set = 0; set < nsets; set++) {
+        const hipStream_t st = stream_of(set);
+        HIPCHK(hipStreamWaitEvent(st, b.uploaded, 0));
+        for (int t = 0; t < (int)c->last_foot.size(); t++) {
+            bool overlap = set >= (int)b.foot.size();  // no footprint: wait for everything
+            for (size_t i = 0; !overlap && i < b.foot[set].size(); i++) overlap = c->last_foot[t][b.foot[set][i]];
+            if (overlap) HIPCHK(hipStreamWaitEvent(st, c->sev[t], 0));
+        }
+    }
+    HIPCHK(hipEventRecord(H.b[0], stream_of(0)));
     for (int i = 0; i < nl; i++) {
         const hipStream_t st = stream_of(launches[i].set);
         a.slice_base = launches[i].begin;
@@ -541,10 +571,13 @@ extern "C" int mp2vg_batch_decode(mp2vg_ctx_t* c) {
         if (a.nslices) HIPCHK(launch_recon(c->g.cf, launches[i].mcm, a, st));
         if (c->launch_timing) HIPCHK(hipEventRecord(H.l[2 * i + 1], st));
     }
-    for (int set = 1; set < nsets; set++) {
-        HIPCHK(hipEventRecord(c->sev[set - 1], stream_of(set)));
-        HIPCHK(hipStreamWaitEvent(c->stream, c->sev[set - 1], 0));
+    for (int set = 0; set < nsets; set++) {
+        HIPCHK(hipEventRecord(c->sev[set], stream_of(set)));
+        HIPCHK(hipStreamWaitEvent(c->stream, c->sev[set], 0));
     }
+    c->last_foot.assign(nsets, std::vector<uint8_t>(c->nslots, 0));
+    for (int set = 0; set < nsets && set < (int)b.foot.size(); set++)
+        for (int32_t x : b.foot[set]) c->last_foot[set][x] = 1;
     HIPCHK(hipEventRecord(H.b[1], c->stream));
     HIPCHK(hipEventRecord(b.consumed, c->stream));
     b.decoded = true;
@@ -574,6 +607,20 @@ extern "C" int mp2vg_batch_times(mp2vg_ctx_t* c, int32_t back, float* batch_ms, 
     if (count) *count = H.nl;
     for (int i = 0; launch_ms && i < H.nl && i < max; i++)
         HIPCHK(hipEventElapsedTime(&launch_ms[i], H.l[2 * i], H.l[2 * i + 1]));
+    return MP2VG_OK;
+}
+
+extern "C" int mp2vg_batches_span(mp2vg_ctx_t* c, int32_t back_first, int32_t back_last, float* ms) {
+    if (!c || !ms || back_last < 0 || back_first < back_last) return MP2VG_E_INVALID;
+    if ((uint64_t)back_first >= c->seq || back_first >= mp2vg_ctx::kHist) {
+        set_error("no such decoded batch (mp2vg_batch_times keeps the last 64)");
+        return MP2VG_E_STATE;
+    }
+    HIPCHK(hipSetDevice(c->cfg.device));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    const mp2vg_ctx::BatchEv& A = c->hist[(c->seq - 1 - (uint64_t)back_first) % mp2vg_ctx::kHist];
+    const mp2vg_ctx::BatchEv& B = c->hist[(c->seq - 1 - (uint64_t)back_last) % mp2vg_ctx::kHist];
+    HIPCHK(hipEventElapsedTime(ms, A.b[0], B.b[1]));
     return MP2VG_OK;
 }
 

@@ -178,6 +178,13 @@ class DeviceContext:
         check(lib().mp2vg_batch_times(self.h, int(back), ctypes.byref(ms), buf, 256, ctypes.byref(n)), "batch_times")
         return ms.value, list(buf[:min(n.value, 256)])
 
+    def batches_span(self, back_first, back_last=0):
+        """Device ms from the start of the batch decoded `back_first` decodes ago to the end of the
+        one `back_last` decodes ago (back-to-back batches overlap set by set)."""
+        ms = ctypes.c_float()
+        check(lib().mp2vg_batches_span(self.h, int(back_first), int(back_last), ctypes.byref(ms)), "batches_span")
+        return ms.value
+
     def download(self, slot):
         """Visible planes of one slot: [Y, U, V] numpy arrays (height x width)."""
         planes = [np.empty((self.ph[i], self.pw[i]), np.uint8) for i in range(3)]
