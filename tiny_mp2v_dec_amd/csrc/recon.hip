@@ -572,38 +572,34 @@ __device__ __forceinline__ uint32_t dq_entry(const Group& S, int lane) {
 // non-intra arithmetic.
 template <int CF, bool INTRA_ONLY = false>
 __device__ __forceinline__ void dequant_word(Lds<CF>& L, int wave, const Group& S, uint32_t w) {
-    const int k = (int)(((w >> 28) - S.x0) & 7u);  // MB column bits (include/mp2vg.h), checked on upload
-    const int bb = (w >> 22) & 15;
-    const uint32_t e = L.dq[wave][(k & 3) * 16 + bb];
-    if (k > 3 || !(e & (1u << 19))) return;  // host validation rejects these
+    // the word's MB in its group: slices are whole MB rows (plan_batch), so groups start at a
+    // column multiple of 4 and the MB is (column mod 8) & 3 = bits 28-29; block bits 22-25.  A
+    // word's block is coded in its MB's cbp (mp2vg_batch_upload rejects batches where not).
+    (void)S;
+    const uint32_t e = L.dq[wave][((w >> 24) & 0x30u) | ((w >> 22) & 0xFu)];
     const int slot = (int)(e & 0xff);
     const bool intra = INTRA_ONLY || ((e >> 18) & 1);
     const int qs = (int)((e >> 8) & 0xff);
     const int i = (w >> 16) & 63;
     const int level = (short)(w & 0xffff);
-    if (w & MP2VG_COEF_DC) {  // QFS[0] = dc << (3 - prec), outside the parity sum (:160)
-        L.blk[wave][slot][0] = (short)level;
-        return;
-    }
+    const bool dc = w & MP2VG_COEF_DC;  // QFS[0] = dc << (3 - prec), outside the parity sum (:160)
+    const bool s1 = !INTRA_ONLY && (w & MP2VG_COEF_FIRST1S);
     const int Wi = L.W[(e >> 16) & 3][i];
     const int sign = level < 0 ? -1 : 0;
     const int mag = level < 0 ? -level : level;
     // W*qs < 2^16 and 2*|level|+1 <= 65537 < 2^24: 24-bit multiplies (full rate) give the low 32
     // bits of the product, i.e. the reference's int arithmetic, where v_mul_lo_u32 is quarter rate
     const uint32_t wq = __umul24((uint32_t)Wi, (uint32_t)qs);
-    short v;
-    int pos;
-    if (!INTRA_ONLY && (w & MP2VG_COEF_FIRST1S)) {  // (3*W*qs)>>5 at qfs[0], unclamped (:79-88)
-        const short t = (short)((int)(3u * wq) >> 5);
-        v = (short)((t ^ sign) - sign);
-        pos = 0;
-    } else {
-        int val = intra ? (int)mul24_asm((uint32_t)mag, wq) >> 4 : (int)mul24_asm((uint32_t)(2 * mag + 1), wq) >> 5;
-        val = (val ^ sign) - sign;
-        const int t = (short)val;  // int16 truncation before the clamp (:146)
-        v = (short)min(max(t, -2048), 2047);  // v_med3_i32
-        pos = L.scan[i];
+    int val = intra ? (int)mul24_asm((uint32_t)mag, wq) >> 4 : (int)mul24_asm((uint32_t)(2 * mag + 1), wq) >> 5;
+    val = (val ^ sign) - sign;
+    const int t = (short)val;  // int16 truncation before the clamp (:146)
+    short v = (short)min(max(t, -2048), 2047);  // v_med3_i32
+    if (!INTRA_ONLY) {  // '1s' first coefficient: (3*W*qs)>>5 at qfs[0], unclamped (:79-88)
+        const short t1 = (short)((int)(3u * wq) >> 5);
+        v = s1 ? (short)((t1 ^ sign) - sign) : v;
     }
+    v = dc ? (short)level : v;  // branch-free: every lane of the word round writes once
+    const int pos = (dc || s1) ? 0 : (int)L.scan[i];
     L.blk[wave][slot][pos] = v;
 }
 

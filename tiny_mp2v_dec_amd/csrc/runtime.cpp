@@ -264,10 +264,15 @@ static int plan_batch(mp2vg_ctx_t* c, const mp2vg_picture_t* pics, int32_t npics
             if ((uint64_t)m.coef_off + m.ncoef > ncoefs) return "MB coefficient range outside the batch";
             // the kernel takes a word's MB (inside its 8-MB group) from bits 28-30
             const uint32_t tag = MP2VG_COEF_MBX(m.x);
-            uint32_t bad = 0;
+            uint32_t bad = 0, blocks = 0;
             const uint32_t* w = coefs + m.coef_off;
-            for (uint32_t j = 0; j < m.ncoef; j++) bad |= (w[j] & 0xF0000000u) ^ tag;
+            for (uint32_t j = 0; j < m.ncoef; j++) {
+                bad |= (w[j] & 0xF0000000u) ^ tag;
+                blocks |= 1u << MP2VG_COEF_BLOCK(w[j]);
+            }
             if (bad) return "coefficient word bits 28-31 are not the MB column mod 8";
+            // the kernel files a word under its block's coded-block slot: the block must be coded
+            if (blocks & ~(uint32_t)m.cbp) return "coefficient word of a block the MB's cbp does not code";
             // the kernel streams the coefficient words of consecutive MBs of a row as one range
             if (k % mbw != 0) {
                 const mp2vg_mb_t& pm = mbs[P.mb_first + k - 1];
