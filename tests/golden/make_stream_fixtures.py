@@ -46,6 +46,15 @@ CASES = [
     ("mc_heavy_fcode1", 176, 144, 1, dict(n_gops=1, gop_n=12, gop_m=3, f_code=1, mix=2, seed=1738)),
     ("tall_2816_vpos_ext", 64, 2816, 1, dict(n_gops=1, gop_n=4, gop_m=3, leading_b=0, seed=1739)),
     ("hd1080_420_ipb", 1920, 1088, 1, dict(n_gops=1, gop_n=4, gop_m=3, leading_b=0, seed=1740)),
+    # high-bitrate intra: I-picture blocks of 18-50 coefficients (up to 200 per mille escape-sized
+    # levels), in both scans, next to P/B pictures, in every chroma format
+    ("intra444_dense", 176, 144, 3, dict(n_gops=1, gop_n=3, gop_m=1, mix=1, intra_coefs_min=20,
+                                          intra_coefs_max=40, alternate_scan=-1, seed=1742)),
+    ("intra422_dense_alt", 352, 288, 2, dict(n_gops=1, gop_n=2, gop_m=1, mix=1, intra_coefs_min=18,
+                                              intra_coefs_max=50, alternate_scan=1, big_level_permille=200,
+                                              seed=1743)),
+    ("ipb420_dense_i", 176, 144, 1, dict(n_gops=2, gop_n=6, gop_m=3, intra_coefs_min=20, intra_coefs_max=40,
+                                          alternate_scan=-1, seed=1744)),
 ]
 
 
