@@ -30,23 +30,30 @@ __device__ __forceinline__ short2_t subs2(short2_t a, short2_t b) { return __bui
 __device__ __forceinline__ short2_t shl2(short2_t a, int n) {
     return __builtin_bit_cast(short2_t, __builtin_bit_cast(ushort2, a) << (unsigned short)n);
 }
+// _mm_mulhi_epi16 on a packed pair: two 24-bit products (SDWA word selects, full rate) and one
+// v_perm of their high halves
 __device__ __forceinline__ short2_t mulhi2(short2_t a, int c) {
-    short2_t r;
-    r.x = (short)(((int)a.x * c) >> 16);
-    r.y = (short)(((int)a.y * c) >> 16);
-    return r;
+    const uint32_t u = __builtin_bit_cast(uint32_t, a);
+    const int lo = (int)(short)(u & 0xffffu) * c, hi = ((int)u >> 16) * c;
+    return __builtin_bit_cast(short2_t, __builtin_amdgcn_perm((uint32_t)hi, (uint32_t)lo, 0x07060302u));
+}
+// _mm_slli_epi16(_mm_mulhi_epi16(a, c), 1) = high halves of a*2c with bit 0 cleared: one perm and
+// one AND instead of two shifts, a perm and an AND
+__device__ __forceinline__ short2_t mulhi2_x2(short2_t a, int c) {
+    const short2_t h = mulhi2(a, 2 * c);
+    return __builtin_bit_cast(short2_t, __builtin_bit_cast(uint32_t, h) & 0xfffefffeu);
 }
 
 // idct_sse2.hpp:23-65, two lanes of the SSE2 vector at once
 __device__ __forceinline__ void idct_1d(short2_t s[8]) {
-    const short2_t v15 = adds2(shl2(mulhi2(s[0], 27145), 1), shl2(s[0], 1));
+    const short2_t v15 = adds2(mulhi2_x2(s[0], 27145), shl2(s[0], 1));
     const short2_t v26 = adds2(mulhi2(s[1], -5037), shl2(s[1], 2));
     const short2_t v21 = adds2(mulhi2(s[2], -19954), shl2(s[2], 2));
-    const short2_t v28 = adds2(shl2(mulhi2(s[3], -22089), 1), shl2(s[3], 2));
-    const short2_t v16 = adds2(shl2(mulhi2(s[4], 27145), 1), shl2(s[4], 1));
+    const short2_t v28 = adds2(mulhi2_x2(s[3], -22089), shl2(s[3], 2));
+    const short2_t v16 = adds2(mulhi2_x2(s[4], 27145), shl2(s[4], 1));
     const short2_t v25 = adds2(mulhi2(s[5], 14567), shl2(s[5], 1));
-    const short2_t v22 = adds2(shl2(mulhi2(s[6], 17391), 1), s[6]);
-    const short2_t v27 = shl2(mulhi2(s[7], 25570), 1);
+    const short2_t v22 = adds2(mulhi2_x2(s[6], 17391), s[6]);
+    const short2_t v27 = mulhi2_x2(s[7], 25570);
     const short2_t v19 = subs2(v25, v28);
     const short2_t v20 = subs2(v26, v27);
     const short2_t v23 = adds2(v26, v27);
@@ -768,8 +775,11 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, Lds
             par ^= (uint32_t)__builtin_amdgcn_ds_swizzle((int)par, 0x041F);  // xor lane 1
             par ^= (uint32_t)__builtin_amdgcn_ds_swizzle((int)par, 0x081F);  // xor lane 2
             if (v == 6) rb.w ^= (par ^ 1u) << 16;  // sum even -> toggle the LSB of QFS[63]
-            short2_t s[8];
-            interleave(ra, rb, s);
+            // pair-interleaved block: dword u = (row v, row v + 1) of column u, no unpacking
+            short2_t s[8] = {__builtin_bit_cast(short2_t, ra.x), __builtin_bit_cast(short2_t, ra.y),
+                             __builtin_bit_cast(short2_t, ra.z), __builtin_bit_cast(short2_t, ra.w),
+                             __builtin_bit_cast(short2_t, rb.x), __builtin_bit_cast(short2_t, rb.y),
+                             __builtin_bit_cast(short2_t, rb.z), __builtin_bit_cast(short2_t, rb.w)};
             idct_1d(s);
 #pragma unroll
             for (int x = 0; x < 8; x++) *(short2_t*)&L.blk[wave][slot][x * 8 + v] = s[x];
@@ -850,7 +860,10 @@ __global__ __launch_bounds__(256) void recon_kernel(const mp2vg_picture_t* __res
 
     if (tid < 64) {
         ((uint32_t*)L.W)[tid] = ((const uint32_t*)pic->W)[tid];
-        L.scan[tid] = c_scan_raster[alt][tid];
+        // blocks sit in LDS pair-interleaved: coefficient (v, u) at (v >> 1) * 16 + u * 2 + (v & 1),
+        // so a dword is the (row v, row v + 1) pair of column u that IDCT pass 1 transforms
+        const int r = c_scan_raster[alt][tid];
+        L.scan[tid] = (uint8_t)((r >> 4) * 16 + (r & 7) * 2 + ((r >> 3) & 1));
     }
     for (int i = lane; i < Lds<CF>::MAXS * BLKS / 2; i += 64) ((uint32_t*)L.blk[wave])[i] = 0;
     __syncthreads();
