@@ -81,18 +81,18 @@ typedef struct mp2vg_mb {
 
 /* Coefficient word: bits 0-15 int16 level (signed run-level level, or the final QFS[0] value
  * when MP2VG_COEF_DC), bits 16-21 scan position i (0..63), bits 22-25 block index (0..11),
- * bit 26 FIRST1S: non-intra first coefficient coded with the B.14 '1s' code — dequantised as
- * (3*W[0]*qs)>>5 without the +-2047 clamp (mb_decoder.cpp:79-88), bit 27 DC: intra DC value,
- * excluded from the mismatch parity (mb_decoder.cpp:76,160), bits 28-30: the MB's column x
- * mod 8 (the kernel finds a word's MB in its 4-MB group from it; mp2vg_batch_upload
- * validates it), bit 31: 0.
+ * bits 26-28: the MB's column x mod 8 (bits 22-27 are the word's (MB in its 4-MB group, block)
+ * index for the kernel; mp2vg_batch_upload validates them), bit 29 FIRST1S: non-intra first
+ * coefficient coded with the B.14 '1s' code — dequantised as (3*W[0]*qs)>>5 without the
+ * +-2047 clamp (mb_decoder.cpp:79-88), bit 30 DC: intra DC value, excluded from the mismatch
+ * parity (mb_decoder.cpp:76,160), bit 31: 0.  FIRST1S and DC words carry i = 0.
  * Words of one MB are grouped by block, blocks in bitstream order.                           */
 #define MP2VG_COEF_LEVEL(w) ((int16_t)((w) & 0xffffu))
 #define MP2VG_COEF_POS(w) (((w) >> 16) & 63u)
 #define MP2VG_COEF_BLOCK(w) (((w) >> 22) & 15u)
-#define MP2VG_COEF_FIRST1S (1u << 26)
-#define MP2VG_COEF_DC (1u << 27)
-#define MP2VG_COEF_MBX(x) (((uint32_t)(x) & 7u) << 28)
+#define MP2VG_COEF_FIRST1S (1u << 29)
+#define MP2VG_COEF_DC (1u << 30)
+#define MP2VG_COEF_MBX(x) (((uint32_t)(x) & 7u) << 26)
 #define MP2VG_COEF_PACK(level, pos, block, fl) \
     ((uint32_t)(uint16_t)(int16_t)(level) | ((uint32_t)(pos) << 16) | ((uint32_t)(block) << 22) | (uint32_t)(fl))
 

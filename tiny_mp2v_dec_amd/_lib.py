@@ -22,7 +22,7 @@ PIC_DTYPE = np.dtype([("dst_slot", "<i4"), ("fwd_slot", "<i4"), ("bwd_slot", "<i
 assert PIC_DTYPE.itemsize == 288
 
 MB_INTRA, MB_FWD, MB_BWD, MB_FIELD_MC, MB_DCT_FIELD = 1, 2, 4, 8, 16
-COEF_FIRST1S, COEF_DC = 1 << 26, 1 << 27
+COEF_FIRST1S, COEF_DC = 1 << 29, 1 << 30
 
 
 def mb_fs_bit(r, s):
@@ -30,9 +30,9 @@ def mb_fs_bit(r, s):
 
 
 def coef_pack(level, pos, block, flags=0, mbx=0):
-    """Coefficient word (include/mp2vg.h); mbx = the MB's column (bits 28-30 carry mbx & 7)."""
+    """Coefficient word (include/mp2vg.h); mbx = the MB's column (bits 26-28 carry mbx & 7)."""
     return (np.uint32(np.int64(level) & 0xFFFF) | np.uint32(pos << 16) | np.uint32(block << 22) |
-            np.uint32(flags) | np.uint32((int(mbx) & 7) << 28))
+            np.uint32(flags) | np.uint32((int(mbx) & 7) << 26))
 
 
 STATUS = {0: "ok", -1: "invalid argument", -2: "unsupported stream", -3: "HIP error", -4: "out of memory",

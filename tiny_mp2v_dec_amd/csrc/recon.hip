@@ -217,7 +217,6 @@ struct Group {
     uint32_t qs8;           // byte k: quantiser_scale
     uint32_t sb8;           // byte k: first coded-block slot of MB k in the group
     uint32_t cbp01, cbp23;  // 16-bit coded_block_pattern of MBs 0,1 / 2,3 (0 if absent)
-    uint32_t x0;            // column of MB 0 mod 8: a coefficient word's MB is ((w >> 28) - x0) & 7
     int nslots, ncoef;
     uint32_t coef0;
 };
@@ -255,7 +254,6 @@ __device__ __forceinline__ Group group_state(uint32_t rv, int ng) {
     S.nslots = sb;
     S.ncoef = cr;
     S.coef0 = rec_uni<3, 0>(rv);
-    S.x0 = rec_uni<0, 0>(rv) & 7u;
     return S;
 }
 
@@ -578,12 +576,12 @@ __device__ __forceinline__ uint32_t dq_entry(const Group& S, int lane) {
 // dequant entry.  INTRA_ONLY (I pictures: every MB intra, no '1s' first coefficients) drops the
 // non-intra arithmetic.
 template <int CF, bool INTRA_ONLY = false>
-__device__ __forceinline__ void dequant_word(Lds<CF>& L, int wave, const Group& S, uint32_t w) {
+__device__ __forceinline__ void dequant_word(Lds<CF>& L, int wave, uint32_t w) {
     // the word's MB in its group: slices are whole MB rows (plan_batch), so groups start at a
-    // column multiple of 4 and the MB is (column mod 8) & 3 = bits 28-29; block bits 22-25.  A
-    // word's block is coded in its MB's cbp (mp2vg_batch_upload rejects batches where not).
-    (void)S;
-    const uint32_t e = L.dq[wave][((w >> 24) & 0x30u) | ((w >> 22) & 0xFu)];
+    // column multiple of 4 and the MB is (column mod 8) & 3 = bits 26-27, next to the block
+    // (bits 22-25): bits 22-27 index the group's dequant table.  A word's block is coded in its
+    // MB's cbp, and DC / '1s' words carry i = 0 (mp2vg_batch_upload rejects batches where not).
+    const uint32_t e = L.dq[wave][(w >> 22) & 63u];
     const int slot = (int)(e & 0xff);
     const bool intra = INTRA_ONLY || ((e >> 18) & 1);
     const int qs = (int)((e >> 8) & 0xff);
@@ -606,8 +604,7 @@ __device__ __forceinline__ void dequant_word(Lds<CF>& L, int wave, const Group& 
         v = s1 ? (short)((t1 ^ sign) - sign) : v;
     }
     v = dc ? (short)level : v;  // branch-free: every lane of the word round writes once
-    const int pos = (dc || s1) ? 0 : (int)L.scan[i];
-    L.blk[wave][slot][pos] = v;
+    L.blk[wave][slot][L.scan[i]] = v;  // i = 0 for DC and '1s' words: block position 0
 }
 
 // force the wait for every tap load here (an empty asm reading the registers): a direction
@@ -733,7 +730,7 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, Lds
             // words 0..64*NCW-1 from the registers loaded one group ahead; more (rare) loaded here
 #pragma unroll
             for (int j = 0; j < NCW; j++)
-                if (64 * j + lane < S.ncoef) dequant_word<CF, MCM == 0>(L, wave, S, cw[j]);
+                if (64 * j + lane < S.ncoef) dequant_word<CF, MCM == 0>(L, wave, cw[j]);
             // words past the prefetch: XW loads per lane in flight per round trip, not one (a 4:4:4
             // intra group carries ~1,400 words)
             constexpr int XW = MCM == 0 ? 8 : 2;
@@ -746,7 +743,7 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, Lds
                 }
 #pragma unroll
                 for (int j = 0; j < XW; j++)
-                    if (base + 64 * j + lane < S.ncoef) dequant_word<CF, MCM == 0>(L, wave, S, xw[j]);
+                    if (base + 64 * j + lane < S.ncoef) dequant_word<CF, MCM == 0>(L, wave, xw[j]);
             }
         }
         // first 64*NCW coefficient words of g+1 (the words of g are consumed)
@@ -840,8 +837,10 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, Lds
     }
 }
 
+// 4:2:0 / 4:2:2 workgroups fit 4 per CU in LDS: ask for the 4 waves per SIMD that 128 VGPRs
+// allow (4:4:4 fits 3 in LDS, so 168 VGPRs cost nothing)
 template <int CF, int MCM, int ABL = 0>
-__global__ __launch_bounds__(256) void recon_kernel(const mp2vg_picture_t* __restrict__ pics,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CF == 3 ? 3 : 4))) void recon_kernel(const mp2vg_picture_t* __restrict__ pics,
                                                     const uint32_t* __restrict__ mbrec,
                                                     const uint32_t* __restrict__ coefs,
                                                     const SliceDesc* __restrict__ slices,

@@ -262,15 +262,19 @@ static int plan_batch(mp2vg_ctx_t* c, const mp2vg_picture_t* pics, int32_t npics
             const mp2vg_mb_t& m = mbs[P.mb_first + k];
             if (m.x != k % mbw || m.y != k / mbw) return "MB records not in raster order";
             if ((uint64_t)m.coef_off + m.ncoef > ncoefs) return "MB coefficient range outside the batch";
-            // the kernel takes a word's MB (inside its 8-MB group) from bits 28-30
+            // the kernel takes a word's MB (inside its 4-MB group) from bits 26-27, and files DC /
+            // '1s' words under the block position of i, which must be 0
             const uint32_t tag = MP2VG_COEF_MBX(m.x);
-            uint32_t bad = 0, blocks = 0;
+            const uint32_t first = MP2VG_COEF_DC | MP2VG_COEF_FIRST1S;
+            uint32_t bad = 0, blocks = 0, pos0 = 0;
             const uint32_t* w = coefs + m.coef_off;
             for (uint32_t j = 0; j < m.ncoef; j++) {
-                bad |= (w[j] & 0xF0000000u) ^ tag;
+                bad |= (w[j] & 0x9C000000u) ^ tag;
                 blocks |= 1u << MP2VG_COEF_BLOCK(w[j]);
+                pos0 |= (w[j] & first) ? MP2VG_COEF_POS(w[j]) : 0u;
             }
-            if (bad) return "coefficient word bits 28-31 are not the MB column mod 8";
+            if (bad) return "coefficient word bits 26-28 are not the MB column mod 8 (or bit 31 is set)";
+            if (pos0) return "DC or '1s' coefficient word with a nonzero scan position";
             // the kernel files a word under its block's coded-block slot: the block must be coded
             if (blocks & ~(uint32_t)m.cbp) return "coefficient word of a block the MB's cbp does not code";
             // the kernel streams the coefficient words of consecutive MBs of a row as one range

@@ -6,6 +6,6 @@ mkdir -p gpurun_out/$TAG
 timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/$TAG/gpu_tests.log 2>&1
 rc=$?; echo "tests rc=$rc $(tail -1 gpurun_out/$TAG/gpu_tests.log)"
 if [ $rc != 0 ]; then grep -E "FAILED|Error|assert" gpurun_out/$TAG/gpu_tests.log | head -20; exit 1; fi
-for cfg in c2 c5; do
+for cfg in ${CFGS:-c2 c5}; do
   tools/ab_lib.sh "--config $cfg --steps 10 --no-e2e" $R $V | sed "s/^/$cfg /" || exit 1
 done
