@@ -553,6 +553,7 @@ struct SliceCtx {
     // address serialize in one L2 channel, and a wave's first loop-head wait covers its own
     uint8_t* wsink;
     __amdgpu_buffer_rsrc_t ref_fwd, ref_bwd;
+    __amdgpu_buffer_rsrc_t coef_rsrc;  // the batch's words; offsets >= kNoTap read nothing
     uint32_t mb_begin, mb_end;
 };
 
@@ -632,6 +633,24 @@ __device__ __forceinline__ void stamp(Stamps& st, int i) {
     st.t = t;
 }
 
+// the first 64*NCW coefficient words of a group, one per lane per register: P/B groups carry
+// few words (plain loads, the array is padded by 256 words); I groups up to NCW*64 through the
+// batch's coefficient buffer resource, registers wholly past the group's words out of range
+template <int MCM, int NCW>
+__device__ __forceinline__ void prefetch_words(uint32_t (&cw)[NCW], const SliceCtx& c, uint32_t coef0, int ncoef,
+                                               int lane) {
+    if (MCM != 0) {
+#pragma unroll
+        for (int j = 0; j < NCW; j++) cw[j] = c.coefs[coef0 + 64 * j + lane];
+    } else {
+        const uint32_t off = (coef0 + (uint32_t)lane) * 4u;
+#pragma unroll
+        for (int j = 0; j < NCW; j++)
+            cw[j] = __builtin_amdgcn_raw_buffer_load_b32(c.coef_rsrc, 64 * j < ncoef ? (int)(off + 256u * j) : (int)kNoTap,
+                                                         0, 0);
+    }
+}
+
 // Software pipeline per wave, one iteration per group g (the wave's groups are STEP MBs apart):
 //   top:       taps of g have landed (one vmcnt wait) -> prediction P(g) in VGPRs
 //   look-ahead: taps of g+1 (records of g+1 arrived one iteration ago), records of g+2
@@ -656,7 +675,10 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, Lds
     Group S;
     // coefficient words prefetched one group ahead, 64 per register: intra groups (I pictures) carry
     // ~180 words, and a word past the prefetch is a synchronous load (a full memory latency)
-    constexpr int NCW = MCM == 0 ? 4 : 2;
+    // I pictures (MCM 0) prefetch as many words as a dense intra group carries (a 4:4:4 group of
+    // 20-40 AC per block: ~1,500) with range-checked buffer loads: registers past the group's
+    // words load nothing (kNoTap), and no load waits inside the dequant
+    constexpr int NCW = MCM == 0 ? (CF == 3 ? 24 : (CF == 2 ? 12 : 8)) : 2;
     uint32_t gr0, gr1, rvN, cw[NCW];
     bool glive;
     {
@@ -670,8 +692,7 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, Lds
         gr1 = R.r1;
         __builtin_amdgcn_sched_barrier(0);
         rvN = rec_load(c.mbrec, g + STEP < mb_end ? g + STEP : g, mb_last, lane);
-#pragma unroll
-        for (int j = 0; j < NCW; j++) cw[j] = c.coefs[S.coef0 + 64 * j + lane];
+        prefetch_words<MCM, NCW>(cw, c, S.coef0, S.ncoef, lane);
         __builtin_amdgcn_sched_barrier(0);
         if (MCM) {
             issue_pass<CF, MCM, 1, NWC, ABL>(R, glive, lane, geo, c.ref_fwd, c.ref_bwd, t1f, t1b);
@@ -748,8 +769,7 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, Lds
         }
         // first 64*NCW coefficient words of g+1 (the words of g are consumed)
         __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int j = 0; j < NCW; j++) cw[j] = c.coefs[SN.coef0 + 64 * j + lane];
+        prefetch_words<MCM, NCW>(cw, c, SN.coef0, SN.ncoef, lane);
         __builtin_amdgcn_sched_barrier(0);
         wave_sync();
 
@@ -876,6 +896,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CF == 3 ? 3
                           (uint32_t)geo.slot_bytes);
     c.ref_bwd = slot_rsrc(pool + (uint64_t)(pic->bwd_slot < 0 ? pic->dst_slot : pic->bwd_slot) * geo.slot_bytes,
                           (uint32_t)geo.slot_bytes);
+    c.coef_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)coefs, (short)0, (int)kNoTap, 0x00020000);
     c.mb_begin = sd.mb_begin;
     c.mb_end = sd.mb_begin + sd.mb_count;
     if (MCM < 3) {
