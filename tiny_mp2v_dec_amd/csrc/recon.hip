@@ -673,11 +673,10 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, Lds
     Tap<NWC> t1f, t1b;  // chroma rows (4:2:0: Cb + Cr; else Cb)
     Tap<NWC> t2f, t2b;  // Cr rows (4:2:2 / 4:4:4)
     Group S;
-    // coefficient words prefetched one group ahead, 64 per register: intra groups (I pictures) carry
-    // ~180 words, and a word past the prefetch is a synchronous load (a full memory latency)
-    // I pictures (MCM 0) prefetch as many words as a dense intra group carries (a 4:4:4 group of
-    // 20-40 AC per block: ~1,500) with range-checked buffer loads: registers past the group's
-    // words load nothing (kNoTap), and no load waits inside the dequant
+    // coefficient words prefetched one group ahead, 64 per register; a word past the prefetch is a
+    // synchronous load (a full memory latency).  I pictures (MCM 0) prefetch as many words as a
+    // dense intra group carries (4:4:4, 20-40 AC per block: ~1,500; 2,048 measured no faster)
+    // with range-checked buffer loads: registers past the group's words load nothing (kNoTap)
     constexpr int NCW = MCM == 0 ? (CF == 3 ? 24 : (CF == 2 ? 12 : 8)) : 2;
     uint32_t gr0, gr1, rvN, cw[NCW];
     bool glive;
