@@ -60,3 +60,22 @@ def test_malformed_batches_rejected():
     pics = p.pics.copy(); pics[1]["fwd_slot"] = -1; pics[1]["bwd_slot"] = -1
     bad(pics=pics, match="missing reference")
     R.validate_batch(*args, p.pics, p.mbs, p.coefs)
+
+
+def test_intra_record_contract():
+    """The I kernel dequantises every word with the intra rule and, in 4:4:4, stores clamp(residual)
+    with no prediction: an I picture with a non-intra MB, or an intra MB that does not code every
+    block (mb_decoder.cpp codes all blocks of intra MBs), is refused."""
+    p = _parsed(3)
+    first_i = int(np.nonzero(p.pics["picture_coding_type"] == 1)[0][0])
+    mbs = p.mbs.copy()
+    k = int(p.pics[first_i]["mb_first"])
+    mbs["flags"][k] = int(mbs["flags"][k]) & ~_lib.MB_INTRA
+    with pytest.raises(_lib.Mp2vgError, match="non-intra macroblock in an I picture"):
+        R.validate_batch(p.width, p.height, 3, p.npics, p.pics, mbs, p.coefs)
+    mbs = p.mbs.copy()
+    partial = np.nonzero((mbs["flags"] & _lib.MB_INTRA == 0) & (mbs["cbp"] != 0) & (mbs["cbp"] != 0xFFF))[0]
+    assert len(partial)
+    mbs["flags"][partial[0]] |= _lib.MB_INTRA
+    with pytest.raises(_lib.Mp2vgError, match="intra macroblock whose cbp"):
+        R.validate_batch(p.width, p.height, 3, p.npics, p.pics, mbs, p.coefs)

@@ -530,19 +530,46 @@ __device__ __forceinline__ void store_pass(uint32_t r0, uint32_t r1, bool live, 
     }
 }
 
+// C8 (4:4:4 I kernel): the row's clamped pixels from the byte residual image, reordered from
+// the ResLayout order (x0, x0+2, x0+1, x0+3 in each 4-pixel group) by one v_perm per dword
+template <int CF, int J>
+__device__ __forceinline__ void store_pass_put8(uint32_t r0, bool live, int lane, const Geo& geo, uint8_t* wsink,
+                                                uint8_t* dst_slot, const uint8_t* res8_wave) {
+    static_assert(CF == 3, "16-pixel rows in every plane");
+    using RL = ResLayout<CF>;
+    int k, plane, py;
+    pass_row<CF, J>(lane, k, plane, py);
+    const uint4 q = *(const uint4*)&res8_wave[k * RL::SIZE + RL::base(plane) + py * 16];
+    const uint4 out = make_uint4(__builtin_amdgcn_perm(q.x, q.x, 0x03010200u), __builtin_amdgcn_perm(q.y, q.y, 0x03010200u),
+                                 __builtin_amdgcn_perm(q.z, q.z, 0x03010200u), __builtin_amdgcn_perm(q.w, q.w, 0x03010200u));
+    uint8_t* dst = dst_slot + gsel(geo.plane_off, plane) +
+                   mul24_asm((r0 >> 16) * 16u + py, (uint32_t)gsel(geo.stride, plane)) + (int)(r0 & 0xffff) * 16;
+    dst = live ? dst : wsink;  // branch-free: every lane stores (see Tap)
+    *(uint4*)dst = out;
+}
+
 // ---- one slice ------------------------------------------------------------------------------
 constexpr int BLKS = 72;
-template <int CF>
+// C8 = the compact layout of the 4:4:4 I kernel: 38.4 KB instead of 53.8 KB per workgroup, so
+// four workgroups (16 waves) share a CU instead of three
+template <int CF, bool C8 = false>
 struct Lds {
+    static constexpr bool COMPACT = C8;
     static constexpr int MAXS = G * Fmt<CF>::NB;  // coded-block slots per group
-    // coef raster -> pass-1 out; slots 144 B apart (BLKS shorts): the transposed pass-1 writes of
-    // the 8 slots in a 32-lane half then hit distinct banks (128 B apart: 8-way conflicts)
-    short blk[WAVES][MAXS][BLKS];
-    short res[WAVES][G * ResLayout<CF>::SIZE];
+    // coef raster -> pass-1 out.  Slots 144 B apart (BLK = 72 shorts): the transposed pass-1
+    // writes of the 8 slots in a 32-lane half then hit distinct banks (128 B apart: 8-way
+    // conflicts).  C8: slots 128 B apart with the 16-B chunk index XOR (slot & 7), same banks.
+    static constexpr int BLK = C8 ? 64 : BLKS;
+    short blk[WAVES][MAXS][BLK];
+    // residual images, int16 in ResLayout; C8 (intra only: output = clamp(residual)): the clamped
+    // pixels as bytes in the same ResLayout order, half the size
+    short res[WAVES][C8 ? G * ResLayout<CF>::SIZE / 2 : G * ResLayout<CF>::SIZE];
     uint8_t map[WAVES][MAXS];                    // slot -> k*16 + b
     uint32_t dq[WAVES][64];                      // (k*16 + b) -> dequant parameters (DqEntry)
     uint8_t W[4][64];
     uint8_t scan[64];
+    // short index of coefficient / pass-1 output idx (0..63) of a slot, relative to the wave's blk
+    __device__ static int bofs(int slot, int idx) { return slot * BLK + (C8 ? (idx ^ ((slot & 7) << 3)) : idx); }
 };
 
 struct SliceCtx {
@@ -576,8 +603,8 @@ __device__ __forceinline__ uint32_t dq_entry(const Group& S, int lane) {
 // slot: lane = word; its MB k (from the word's MB-column bits) and block select the group's
 // dequant entry.  INTRA_ONLY (I pictures: every MB intra, no '1s' first coefficients) drops the
 // non-intra arithmetic.
-template <int CF, bool INTRA_ONLY = false>
-__device__ __forceinline__ void dequant_word(Lds<CF>& L, int wave, uint32_t w) {
+template <class LT, bool INTRA_ONLY = false>
+__device__ __forceinline__ void dequant_word(LT& L, int wave, uint32_t w) {
     // the word's MB in its group: slices are whole MB rows (plan_batch), so groups start at a
     // column multiple of 4 and the MB is (column mod 8) & 3 = bits 26-27, next to the block
     // (bits 22-25): bits 22-27 index the group's dequant table.  A word's block is coded in its
@@ -605,7 +632,7 @@ __device__ __forceinline__ void dequant_word(Lds<CF>& L, int wave, uint32_t w) {
         v = s1 ? (short)((t1 ^ sign) - sign) : v;
     }
     v = dc ? (short)level : v;  // branch-free: every lane of the word round writes once
-    L.blk[wave][slot][L.scan[i]] = v;  // i = 0 for DC and '1s' words: block position 0
+    ((short*)L.blk[wave])[LT::bofs(slot, L.scan[i])] = v;  // i = 0 for DC and '1s' words: block position 0
 }
 
 // force the wait for every tap load here (an empty asm reading the registers): a direction
@@ -658,8 +685,8 @@ __device__ __forceinline__ void prefetch_words(uint32_t (&cw)[NCW], const SliceC
 //   D, E:      IDCT, add/clip + store of g
 // Every look-ahead value is consumed before its register is reloaded (no loop-carried copies of
 // pending loads), so the waits at the top never cover the previous group's stores.
-template <int CF, int MCM, int ABL>
-__device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, Lds<CF>& L, int lane, int wave) {
+template <int CF, int MCM, int ABL, class LT>
+__device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, LT& L, int lane, int wave) {
     using F = Fmt<CF>;
     using RL = ResLayout<CF>;
     constexpr int NB = F::NB;
@@ -750,7 +777,7 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, Lds
             // words 0..64*NCW-1 from the registers loaded one group ahead; more (rare) loaded here
 #pragma unroll
             for (int j = 0; j < NCW; j++)
-                if (64 * j + lane < S.ncoef) dequant_word<CF, MCM == 0>(L, wave, cw[j]);
+                if (64 * j + lane < S.ncoef) dequant_word<LT, MCM == 0>(L, wave, cw[j]);
             // words past the prefetch: XW loads per lane in flight per round trip, not one (a 4:4:4
             // intra group carries ~1,400 words)
             constexpr int XW = MCM == 0 ? 8 : 2;
@@ -763,7 +790,7 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, Lds
                 }
 #pragma unroll
                 for (int j = 0; j < XW; j++)
-                    if (base + 64 * j + lane < S.ncoef) dequant_word<CF, MCM == 0>(L, wave, xw[j]);
+                    if (base + 64 * j + lane < S.ncoef) dequant_word<LT, MCM == 0>(L, wave, xw[j]);
             }
         }
         // first 64*NCW coefficient words of g+1 (the words of g are consumed)
@@ -781,8 +808,9 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, Lds
         //         ds_read instruction before any lane writes it.
         for (int t = lane; t < ((ABL & 1) ? 0 : S.nslots * 4); t += 64) {
             const int slot = t >> 2, v = (t & 3) * 2;
-            uint4 ra = *(const uint4*)&L.blk[wave][slot][v * 8];
-            uint4 rb = *(const uint4*)&L.blk[wave][slot][v * 8 + 8];
+            short* const bw = (short*)L.blk[wave];
+            uint4 ra = *(const uint4*)&bw[LT::bofs(slot, v * 8)];
+            uint4 rb = *(const uint4*)&bw[LT::bofs(slot, v * 8 + 8)];
             const int k = L.map[wave][slot] >> 4;
             const bool intra = pick8(S.fl8, k) & MP2VG_MB_INTRA;
             uint32_t par = (ra.x ^ ra.y ^ ra.z ^ ra.w ^ rb.x ^ rb.y ^ rb.z ^ rb.w) & 0x00010001u;
@@ -798,7 +826,7 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, Lds
                              __builtin_bit_cast(short2_t, rb.z), __builtin_bit_cast(short2_t, rb.w)};
             idct_1d(s);
 #pragma unroll
-            for (int x = 0; x < 8; x++) *(short2_t*)&L.blk[wave][slot][x * 8 + v] = s[x];
+            for (int x = 0; x < 8; x++) *(short2_t*)&bw[LT::bofs(slot, x * 8 + v)] = s[x];
         }
         wave_sync();
         // chroma taps of g+1 issued mid-iteration: spreads the wave's TA demand
@@ -815,10 +843,11 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, Lds
         for (int t = lane; t < ((ABL & 1) ? 0 : S.nslots * 4); t += 64) {
             const int slot = t >> 2, xq = t & 3;
             const int x = (xq & 1) | ((xq & 2) << 1);  // 0, 1, 4, 5
-            const uint4 ra = *(const uint4*)&L.blk[wave][slot][x * 8];
-            const uint4 rb = *(const uint4*)&L.blk[wave][slot][x * 8 + 16];
-            *(uint4*)&L.blk[wave][slot][x * 8] = make_uint4(0, 0, 0, 0);
-            *(uint4*)&L.blk[wave][slot][x * 8 + 16] = make_uint4(0, 0, 0, 0);
+            short* const bw = (short*)L.blk[wave];
+            const uint4 ra = *(const uint4*)&bw[LT::bofs(slot, x * 8)];
+            const uint4 rb = *(const uint4*)&bw[LT::bofs(slot, x * 8 + 16)];
+            *(uint4*)&bw[LT::bofs(slot, x * 8)] = make_uint4(0, 0, 0, 0);
+            *(uint4*)&bw[LT::bofs(slot, x * 8 + 16)] = make_uint4(0, 0, 0, 0);
             short2_t s[8];
             interleave(ra, rb, s);
             idct_1d(s);
@@ -827,19 +856,38 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, Lds
             const bool dctf = pick8(S.fl8, k) & MP2VG_MB_DCT_FIELD;
             int plane, x0, y0, ys;
             block_origin<CF>(bb, dctf, plane, x0, y0, ys);
-            short* res = &L.res[wave][k * RL::SIZE + RL::base(plane)];
             const int rw = RL::width(plane);
             const int xp = RL::pos(x0 + x);  // (x, x+2) -> (xp, xp+1)
+            if constexpr (LT::COMPACT) {
+                // intra put (idct_sse2.hpp:106-108): packus(res) -- the clamped bytes of (x, x+2)
+                uint8_t* res8 = (uint8_t*)L.res[wave] + k * RL::SIZE + RL::base(plane);
+                const short2_t z = {0, 0}, m = {255, 255};
 #pragma unroll
-            for (int y = 0; y < 8; y++) *(short2_t*)&res[(y0 + y * ys) * rw + xp] = s[y] >> (short)6;
+                for (int y = 0; y < 8; y++) {
+                    const short2_t t = __builtin_elementwise_min(__builtin_elementwise_max(s[y] >> (short)6, z), m);
+                    *(uint16_t*)&res8[(y0 + y * ys) * rw + xp] =
+                        (uint16_t)__builtin_amdgcn_perm(0u, __builtin_bit_cast(uint32_t, t), 0x0c0c0200u);
+                }
+            } else {
+                short* res = &L.res[wave][k * RL::SIZE + RL::base(plane)];
+#pragma unroll
+                for (int y = 0; y < 8; y++) *(short2_t*)&res[(y0 + y * ys) * rw + xp] = s[y] >> (short)6;
+            }
         }
         wave_sync();
 
         stamp<ABL>(st, 4);
         // ---- E. prediction + residual, one row store per lane ----
-        store_pass<CF, 0, 4, ABL>(gr0, gr1, glive, lane, geo, c.wsink, c.dst_slot, L.res[wave], p0);
-        store_pass<CF, 1, NWC, ABL>(gr0, gr1, glive, lane, geo, c.wsink, c.dst_slot, L.res[wave], p1);
-        if (CF != 1) store_pass<CF, 2, NWC, ABL>(gr0, gr1, glive, lane, geo, c.wsink, c.dst_slot, L.res[wave], p2);
+        if constexpr (LT::COMPACT) {
+            const uint8_t* res8 = (const uint8_t*)L.res[wave];
+            store_pass_put8<CF, 0>(gr0, glive, lane, geo, c.wsink, c.dst_slot, res8);
+            store_pass_put8<CF, 1>(gr0, glive, lane, geo, c.wsink, c.dst_slot, res8);
+            store_pass_put8<CF, 2>(gr0, glive, lane, geo, c.wsink, c.dst_slot, res8);
+        } else {
+            store_pass<CF, 0, 4, ABL>(gr0, gr1, glive, lane, geo, c.wsink, c.dst_slot, L.res[wave], p0);
+            store_pass<CF, 1, NWC, ABL>(gr0, gr1, glive, lane, geo, c.wsink, c.dst_slot, L.res[wave], p1);
+            if (CF != 1) store_pass<CF, 2, NWC, ABL>(gr0, gr1, glive, lane, geo, c.wsink, c.dst_slot, L.res[wave], p2);
+        }
         wave_sync();
 
         stamp<ABL>(st, 5);
@@ -856,16 +904,17 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, Lds
     }
 }
 
-// 4:2:0 / 4:2:2 workgroups fit 4 per CU in LDS: ask for the 4 waves per SIMD that 128 VGPRs
-// allow (4:4:4 fits 3 in LDS, so 168 VGPRs cost nothing)
+// 4:2:0 / 4:2:2 workgroups and the compact 4:4:4 I kernel fit 4 per CU in LDS: ask for the 4
+// waves per SIMD that 128 VGPRs allow (4:4:4 P/B fit 3, so 168 VGPRs cost nothing)
 template <int CF, int MCM, int ABL = 0>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CF == 3 ? 3 : 4))) void recon_kernel(const mp2vg_picture_t* __restrict__ pics,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CF == 3 && MCM != 0 ? 3 : 4))) void recon_kernel(const mp2vg_picture_t* __restrict__ pics,
                                                     const uint32_t* __restrict__ mbrec,
                                                     const uint32_t* __restrict__ coefs,
                                                     const SliceDesc* __restrict__ slices,
                                                     uint8_t* __restrict__ pool, const Geo geo,
                                                     const uint32_t slice_base, const uint32_t nslices) {
-    __shared__ __attribute__((aligned(16))) Lds<CF> L;
+    using LT = Lds<CF, CF == 3 && MCM == 0 && ABL == 0>;
+    __shared__ __attribute__((aligned(16))) LT L;
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -883,7 +932,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CF == 3 ? 3
         const int r = c_scan_raster[alt][tid];
         L.scan[tid] = (uint8_t)((r >> 4) * 16 + (r & 7) * 2 + ((r >> 3) & 1));
     }
-    for (int i = lane; i < Lds<CF>::MAXS * BLKS / 2; i += 64) ((uint32_t*)L.blk[wave])[i] = 0;
+    for (int i = lane; i < LT::MAXS * LT::BLK / 2; i += 64) ((uint32_t*)L.blk[wave])[i] = 0;
     __syncthreads();
 
     SliceCtx c;
@@ -899,15 +948,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CF == 3 ? 3
     c.mb_begin = sd.mb_begin;
     c.mb_end = sd.mb_begin + sd.mb_count;
     if (MCM < 3) {
-        run_slice<CF, (ABL & 2) ? 0 : MCM, ABL>(c, geo, L, lane, wave);
+        run_slice<CF, (ABL & 2) ? 0 : MCM, ABL, LT>(c, geo, L, lane, wave);
     } else {  // mixed level: the picture type picks the specialised loop (uniform per workgroup)
         const int pct = pic->picture_coding_type;
         if (pct == 3)
-            run_slice<CF, (ABL & 2) ? 0 : 2, ABL>(c, geo, L, lane, wave);
+            run_slice<CF, (ABL & 2) ? 0 : 2, ABL, LT>(c, geo, L, lane, wave);
         else if (pct == 2)
-            run_slice<CF, (ABL & 2) ? 0 : 1, ABL>(c, geo, L, lane, wave);
+            run_slice<CF, (ABL & 2) ? 0 : 1, ABL, LT>(c, geo, L, lane, wave);
         else
-            run_slice<CF, 0, ABL>(c, geo, L, lane, wave);
+            run_slice<CF, 0, ABL, LT>(c, geo, L, lane, wave);
     }
 }
 // Order-independent 64-bit digest of a slot's visible planes:

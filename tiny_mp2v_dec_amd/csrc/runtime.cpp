@@ -290,6 +290,11 @@ static int plan_batch(mp2vg_ctx_t* c, const mp2vg_picture_t* pics, int32_t npics
             // streams, and no record producer may hand them to the kernel (spec placement)
             if (nb == 12 && (m.flags & MP2VG_MB_DCT_FIELD) && m.cbp)
                 return "4:4:4 field-DCT macroblock (reference block 10/11 placement is unsupported)";
+            // intra MBs code every block (the I kernel's 4:4:4 store writes clamp(residual) with
+            // no prediction underneath), and the I kernel dequantises every word as intra
+            if ((m.flags & MP2VG_MB_INTRA) && m.cbp != (1u << nb) - 1)
+                return "intra macroblock whose cbp does not code every block";
+            if (P.picture_coding_type == 1 && !(m.flags & MP2VG_MB_INTRA)) return "non-intra macroblock in an I picture";
             if (!(m.flags & MP2VG_MB_INTRA)) {
                 uses[0] |= (m.flags & MP2VG_MB_FWD) || !(m.flags & MP2VG_MB_BWD);
                 uses[1] |= (m.flags & MP2VG_MB_BWD) != 0;
