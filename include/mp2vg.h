@@ -58,7 +58,8 @@ enum {
  * (mb_decoder.cpp:198-206).
  */
 enum {
-    MP2VG_MB_INTRA = 1u << 0,     /* IDCT put, no MC                                         */
+    MP2VG_MB_INTRA = 1u << 0,     /* IDCT put, no MC; cbp codes every block, and every MB of an
+                                     I picture is intra (both checked on upload)               */
     MP2VG_MB_FWD = 1u << 1,       /* forward prediction from fwd_slot                        */
     MP2VG_MB_BWD = 1u << 2,       /* backward prediction from bwd_slot (both bits: bidir avg) */
     MP2VG_MB_FIELD_MC = 1u << 3,  /* frame picture, field prediction: 2 vectors, 16x8 each  */
