@@ -530,22 +530,29 @@ __device__ __forceinline__ void store_pass(uint32_t r0, uint32_t r1, bool live, 
     }
 }
 
-// C8 (4:4:4 I kernel): the row's clamped pixels from the byte residual image, reordered from
-// the ResLayout order (x0, x0+2, x0+1, x0+3 in each 4-pixel group) by one v_perm per dword
-template <int CF, int J>
+// C8 (I kernels): the row's clamped pixels from the byte residual image, reordered from the
+// ResLayout order (x0, x0+2, x0+1, x0+3 in each 4-pixel group) by one v_perm per dword
+template <int CF, int J, int NW>
 __device__ __forceinline__ void store_pass_put8(uint32_t r0, bool live, int lane, const Geo& geo, uint8_t* wsink,
                                                 uint8_t* dst_slot, const uint8_t* res8_wave) {
-    static_assert(CF == 3, "16-pixel rows in every plane");
+    using F = Fmt<CF>;
     using RL = ResLayout<CF>;
     int k, plane, py;
     pass_row<CF, J>(lane, k, plane, py);
-    const uint4 q = *(const uint4*)&res8_wave[k * RL::SIZE + RL::base(plane) + py * 16];
-    const uint4 out = make_uint4(__builtin_amdgcn_perm(q.x, q.x, 0x03010200u), __builtin_amdgcn_perm(q.y, q.y, 0x03010200u),
-                                 __builtin_amdgcn_perm(q.z, q.z, 0x03010200u), __builtin_amdgcn_perm(q.w, q.w, 0x03010200u));
+    const uint8_t* row = &res8_wave[k * RL::SIZE + RL::base(plane) + py * RL::width(plane)];
+    const int pw = plane == 0 ? 16 : F::CW;
+    const int phm = plane == 0 ? 16 : F::CH;
     uint8_t* dst = dst_slot + gsel(geo.plane_off, plane) +
-                   mul24_asm((r0 >> 16) * 16u + py, (uint32_t)gsel(geo.stride, plane)) + (int)(r0 & 0xffff) * 16;
+                   mul24_asm((r0 >> 16) * phm + py, (uint32_t)gsel(geo.stride, plane)) + (int)(r0 & 0xffff) * pw;
     dst = live ? dst : wsink;  // branch-free: every lane stores (see Tap)
-    *(uint4*)dst = out;
+    if (NW == 4) {
+        const uint4 q = *(const uint4*)row;
+        *(uint4*)dst = make_uint4(__builtin_amdgcn_perm(q.x, q.x, 0x03010200u), __builtin_amdgcn_perm(q.y, q.y, 0x03010200u),
+                                  __builtin_amdgcn_perm(q.z, q.z, 0x03010200u), __builtin_amdgcn_perm(q.w, q.w, 0x03010200u));
+    } else {
+        const uint2 q = *(const uint2*)row;
+        *(uint2*)dst = make_uint2(__builtin_amdgcn_perm(q.x, q.x, 0x03010200u), __builtin_amdgcn_perm(q.y, q.y, 0x03010200u));
+    }
 }
 
 // ---- one slice ------------------------------------------------------------------------------
@@ -880,9 +887,9 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, LT&
         // ---- E. prediction + residual, one row store per lane ----
         if constexpr (LT::COMPACT) {
             const uint8_t* res8 = (const uint8_t*)L.res[wave];
-            store_pass_put8<CF, 0>(gr0, glive, lane, geo, c.wsink, c.dst_slot, res8);
-            store_pass_put8<CF, 1>(gr0, glive, lane, geo, c.wsink, c.dst_slot, res8);
-            store_pass_put8<CF, 2>(gr0, glive, lane, geo, c.wsink, c.dst_slot, res8);
+            store_pass_put8<CF, 0, 4>(gr0, glive, lane, geo, c.wsink, c.dst_slot, res8);
+            store_pass_put8<CF, 1, NWC>(gr0, glive, lane, geo, c.wsink, c.dst_slot, res8);
+            if (CF != 1) store_pass_put8<CF, 2, NWC>(gr0, glive, lane, geo, c.wsink, c.dst_slot, res8);
         } else {
             store_pass<CF, 0, 4, ABL>(gr0, gr1, glive, lane, geo, c.wsink, c.dst_slot, L.res[wave], p0);
             store_pass<CF, 1, NWC, ABL>(gr0, gr1, glive, lane, geo, c.wsink, c.dst_slot, L.res[wave], p1);
@@ -904,16 +911,16 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, LT&
     }
 }
 
-// 4:2:0 / 4:2:2 workgroups and the compact 4:4:4 I kernel fit 4 per CU in LDS: ask for the 4
-// waves per SIMD that 128 VGPRs allow (4:4:4 P/B fit 3, so 168 VGPRs cost nothing)
+// Occupancy targets per kernel from its LDS: 4:2:0 / 4:2:2 P/B workgroups fit 4 per CU (128
+// VGPRs), 4:4:4 P/B 3 (168 VGPRs cost nothing); the compact I kernels fit 4 (4:4:4) or 6 (80 VGPRs)
 template <int CF, int MCM, int ABL = 0>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CF == 3 && MCM != 0 ? 3 : 4))) void recon_kernel(const mp2vg_picture_t* __restrict__ pics,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MCM == 0 ? (CF == 3 ? 4 : 6) : (CF == 3 ? 3 : 4)))) void recon_kernel(const mp2vg_picture_t* __restrict__ pics,
                                                     const uint32_t* __restrict__ mbrec,
                                                     const uint32_t* __restrict__ coefs,
                                                     const SliceDesc* __restrict__ slices,
                                                     uint8_t* __restrict__ pool, const Geo geo,
                                                     const uint32_t slice_base, const uint32_t nslices) {
-    using LT = Lds<CF, CF == 3 && MCM == 0 && ABL == 0>;
+    using LT = Lds<CF, MCM == 0 && ABL == 0>;
     __shared__ __attribute__((aligned(16))) LT L;
     const int tid = threadIdx.x;
     const int lane = tid & 63;
