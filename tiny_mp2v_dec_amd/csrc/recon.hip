@@ -914,7 +914,7 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, LT&
 // Occupancy targets per kernel from its LDS: 4:2:0 / 4:2:2 P/B workgroups fit 4 per CU (128
 // VGPRs), 4:4:4 P/B 3 (168 VGPRs cost nothing); the compact I kernels fit 4 (4:4:4) or 6 (80 VGPRs)
 template <int CF, int MCM, int ABL = 0>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MCM == 0 ? (CF == 3 ? 4 : 6) : (CF == 3 ? 3 : 4)))) void recon_kernel(const mp2vg_picture_t* __restrict__ pics,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MCM == 0 && ABL == 0 ? (CF == 3 ? 4 : 6) : (CF == 3 ? 3 : 4)))) void recon_kernel(const mp2vg_picture_t* __restrict__ pics,
                                                     const uint32_t* __restrict__ mbrec,
                                                     const uint32_t* __restrict__ coefs,
                                                     const SliceDesc* __restrict__ slices,
@@ -1031,11 +1031,17 @@ hipError_t launch_recon(int cf, int mcm, const KArgs& a, hipStream_t stream) {
         g.stride[i] = a.stride[i];
         g.ph[i] = a.ph[i];
     }
-    // development-only ablation switch (MP2VG_ABLATE, 4:2:0 only): 1 no IDCT, 2 no MC, 4 no
-    // dequant, 8 no stores, 16 stage stamps (tools/stamps.py), 32 MC loads out of range (no address
-    // math), 64 no prediction arithmetic, 128 no 17th-pixel dwords, 512 no edge-row loads.
-    // Outputs are wrong under it (except 16); never set in tests or the bench.
+    // development-only ablation switch (MP2VG_ABLATE; compiled only into dev builds with
+    // -DMP2VG_DEV_ABLATIONS, tools/variant.sh EXTRA=...; 4:2:0, and 16 also 4:4:4): 1 no IDCT, 2 no
+    // MC, 4 no dequant, 8 no stores, 16 stage stamps (tools/stamps.py), 32 MC loads out of range
+    // (no address math), 64 no prediction arithmetic, 128 no 17th-pixel dwords, 512 no edge-row
+    // loads, 1024/2048/3072 tiled / all-hit taps, 4096/8192 store shapes.  Outputs are wrong under
+    // it (except 16); never set in tests or the bench.  A product library refuses the variable.
     static const int ablate = getenv("MP2VG_ABLATE") ? atoi(getenv("MP2VG_ABLATE")) : 0;
+#ifndef MP2VG_DEV_ABLATIONS
+    if (ablate) return hipErrorNotSupported;
+#else
+    if (cf == 3 && ablate == 16) return launch_mcm<3, 16>(mcm, a, g, stream);
     if (cf == 1 && ablate) {
         switch (ablate) {
         case 1: return launch_mcm<1, 1>(mcm, a, g, stream);
@@ -1059,6 +1065,7 @@ hipError_t launch_recon(int cf, int mcm, const KArgs& a, hipStream_t stream) {
         default: return hipErrorInvalidValue;
         }
     }
+#endif
     switch (cf) {
     case 1: return launch_mcm<1, 0>(mcm, a, g, stream);
     case 2: return launch_mcm<2, 0>(mcm, a, g, stream);

@@ -1,4 +1,5 @@
 # per-level times of the fused kernel under ablations (MP2VG_ABLATE; wrong output, timing only)
+export MP2VG_LIB=${MP2VG_LIB:-tiny_mp2v_dec_amd/_var/dev/libmp2vg.so}  # tools/dev_build.sh
 set -e
 mkdir -p gpurun_out/fabl
 for a in ${ABLS:-0 8 32}; do

@@ -1,3 +1,4 @@
+export MP2VG_LIB=${MP2VG_LIB:-tiny_mp2v_dec_amd/_var/dev/libmp2vg.so}  # tools/dev_build.sh
 for v in base v8; do
   if [ $v = base ]; then L=""; else L=tiny_mp2v_dec_amd/_var/$v/libmp2vg.so; fi
   for a in 0 1 2 4 8 32 64; do

@@ -1,5 +1,6 @@
 #!/bin/bash
 # Dynamic instruction counts of the recon kernels under each ablation (dev tool, GPU box).
+export MP2VG_LIB=${MP2VG_LIB:-tiny_mp2v_dec_amd/_var/dev/libmp2vg.so}  # tools/dev_build.sh
 set -u
 OUT=gpurun_out/profa_$1; shift
 mkdir -p $OUT

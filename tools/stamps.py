@@ -1,6 +1,7 @@
 """Stage shares of the recon loop from the diagnostic stamp build (MP2VG_ABLATE=16; dev tool).
 
-    MP2VG_ABLATE=16 python tools/stamps.py [--gops 32] [--config c2]
+    tools/dev_build.sh
+    MP2VG_LIB=tiny_mp2v_dec_amd/_var/dev/libmp2vg.so MP2VG_ABLATE=16 python tools/stamps.py [--gops 32] [--config c2]
 Reads the per-mode s_memtime sums the stamp build adds into the pool pad (sink + 1024) and prints
 each stage's share of the loop; quote shares only, never the stamp build's run time.
 """
