@@ -688,7 +688,7 @@ __device__ __forceinline__ void prefetch_words(uint32_t (&cw)[NCW], const SliceC
 // Software pipeline per wave, one iteration per group g (the wave's groups are STEP MBs apart):
 //   top:       taps of g have landed (one vmcnt wait) -> prediction P(g) in VGPRs
 //   look-ahead: taps of g+1 (records of g+1 arrived one iteration ago), records of g+2
-//   C:         dequant of g; then the first 128 coefficient words of g+1
+//   C:         dequant of g; then the coefficient words of g+1 (128; I kernels up to 1,536)
 //   D, E:      IDCT, add/clip + store of g
 // Every look-ahead value is consumed before its register is reloaded (no loop-carried copies of
 // pending loads), so the waits at the top never cover the previous group's stores.
