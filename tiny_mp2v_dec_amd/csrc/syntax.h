@@ -54,6 +54,12 @@ struct BitReader {
         return (uint32_t)(cache >> (64 - n));
     }
     inline void skip(int n) {
+        if (__builtin_expect(n > 32, 0)) return skip_long(n);
+        refill();
+        cache <<= n;
+        bits -= n;
+    }
+    __attribute__((noinline)) void skip_long(int n) {
         while (n > 32) {
             refill();
             cache <<= 32;
@@ -64,9 +70,12 @@ struct BitReader {
         cache <<= n;
         bits -= n;
     }
-    inline uint32_t read(int n) {
-        uint32_t v = peek(n);
-        if (n) skip(n);
+    inline uint32_t read(int n) {  // n <= 32: one refill covers the peek and the skip
+        if (n == 0) return 0;
+        refill();
+        const uint32_t v = (uint32_t)(cache >> (64 - n));
+        cache <<= n;
+        bits -= n;
         return v;
     }
     // No-refill variants for a caller that has just refilled (>= 33 valid bits) and consumes at
@@ -129,10 +138,11 @@ struct VlcLut {
         lut.assign(1u << ml, 0);
     }
     // returns index or -1; consumes the code
-    inline int decode(BitReader& br) const {
-        uint32_t e = lut[br.peek(maxlen)];
+    inline int decode(BitReader& br) const {  // maxlen <= 32: one refill for the peek and the skip
+        br.refill();
+        uint32_t e = lut[br.peek_nr(maxlen)];
         if (!e) return -1;
-        br.skip((int)(e >> 16));
+        br.skip_nr((int)(e >> 16));
         return (int)(e & 0xffff) - 1;
     }
 };
