@@ -79,3 +79,22 @@ def test_intra_record_contract():
     mbs["flags"][partial[0]] |= _lib.MB_INTRA
     with pytest.raises(_lib.Mp2vgError, match="intra macroblock whose cbp"):
         R.validate_batch(p.width, p.height, 3, p.npics, p.pics, mbs, p.coefs)
+
+
+def test_coefficient_array_limit():
+    """The I kernels read coefficient words through a buffer resource with 32-bit byte offsets: a
+    batch of 2^30 or more words is refused before any record is read."""
+    import ctypes
+    p = _parsed(1)
+    cfg = _lib.make_config(p.width, p.height, 1, pool=p.npics)
+    vp = ctypes.c_void_p
+    n = ctypes.c_int32()
+    of_pic = np.zeros(len(p.pics), np.int32)
+    mode = np.zeros(64, np.int32)
+    i32p = ctypes.POINTER(ctypes.c_int32)
+    rc = _lib.lib().mp2vg_batch_validate(ctypes.byref(cfg), p.npics, p.pics.ctypes.data_as(vp), len(p.pics),
+                                         p.mbs.ctypes.data_as(vp), len(p.mbs), p.coefs.ctypes.data_as(vp),
+                                         ctypes.c_uint64(1 << 30), ctypes.byref(n), of_pic.ctypes.data_as(i32p),
+                                         mode.ctypes.data_as(i32p), len(mode))
+    assert rc == -1  # MP2VG_E_INVALID
+    assert "coefficient words" in _lib.lib().mp2vg_last_error().decode()

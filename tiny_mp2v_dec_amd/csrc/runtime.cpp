@@ -243,6 +243,11 @@ static int plan_batch(mp2vg_ctx_t* c, const mp2vg_picture_t* pics, int32_t npics
                       std::vector<Launch>& launches, std::vector<std::vector<int32_t>>* foot = nullptr) {
     const int mbw = c->cfg.width / 16, mbh = c->cfg.height / 16;
     const int nb = c->g.nblocks;
+    // the I kernels address coefficient words with 32-bit byte offsets (a buffer resource)
+    if (ncoefs + kCoefPad >= (1ull << 30)) {
+        set_error("batch with 2^30 or more coefficient words (4 GB): split it");
+        return MP2VG_E_INVALID;
+    }
     std::vector<int> level(npics, 0);
     std::vector<int> last_write(c->nslots, -1), max_read(c->nslots, -1);
     int maxlevel = -1;
