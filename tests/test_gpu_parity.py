@@ -288,3 +288,26 @@ def test_reference_idct_vectors_through_hip():
     bad_put = [j for j in range(n * 6) if not np.array_equal(block(got[0], j // 6, j % 6), put[pidx[j]])]
     bad_add = [j for j in range(n * 6) if not np.array_equal(block(got[1], j // 6, j % 6), add_exp[j])]
     assert not bad_put and not bad_add, (bad_put[:8], bad_add[:8])
+
+
+@pytest.mark.gpu
+def test_product_library_refuses_dev_ablations():
+    """MP2VG_ABLATE (timing-only kernels with wrong output) is compiled only into dev builds
+    (tools/dev_build.sh); the product library fails the decode instead of silently ablating."""
+    import os
+    import subprocess
+    import sys
+    code = ("import sys; sys.path.insert(0, %r)\n"
+            "from tiny_mp2v_dec_amd import records as R\n"
+            "es = R.generate_es(width=64, height=48, chroma_format=1, n_gops=1, gop_n=3, gop_m=1, seed=7)\n"
+            "p = R.Parsed(es, 64, 48, 1)\n"
+            "with R.DeviceContext(64, 48, 1, slots=p.npics) as d:\n"
+            "    d.upload(p.pics, p.mbs, p.coefs)\n"
+            "    try:\n"
+            "        d.decode(); d.synchronize()\n"
+            "    except Exception as e:\n"
+            "        print('refused:', e); sys.exit(0)\n"
+            "sys.exit(5)\n") % os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MP2VG_ABLATE="1")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "refused" in r.stdout, (r.returncode, r.stdout[-500:], r.stderr[-1500:])
