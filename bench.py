@@ -6,7 +6,7 @@ records are already resident in HBM.  Each rank (one per GPU) decodes its own in
 stream (seed 1729 + rank): weak scaling, no data-path collective; RCCL only gathers per-frame
 digests to rank 0 after the timed region (the trivial frame gather).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--gops G] [--config c2|c3|c4|c5]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--gops G] [--config c1|c2|c3|c4|c5]
 
 Prints ONE JSON line on rank 0 (see DESIGN.md "Measurement").
 """
@@ -31,6 +31,9 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
 
 CONFIGS = {
     # name: (width, height, chroma_format, generator params, description)
+    # c1 = BASELINE configs[0]: the reference's own CPU-runnable case (I-only, normal intra bitrate:
+    # 0-12 AC coefficients per block), timed on the reference single-threaded beside the HIP path
+    "c1": (1920, 1088, 1, dict(gop_n=1, gop_m=1, mix=1), "1080p 4:2:0 progressive I-only (120 frames)"),
     "c2": (1920, 1088, 1, dict(gop_n=12, gop_m=3, leading_b=1), "1080p 4:2:0 IPB GOP=12 (N=12, M=3, closed)"),
     "c3": (1920, 1088, 2, dict(gop_n=12, gop_m=3, leading_b=1), "1080p 4:2:2 IPB GOP=12 (N=12, M=3, closed)"),
     "c4": (3840, 2160, 1, dict(gop_n=12, gop_m=3, leading_b=1), "4K 4:2:0 IPB GOP=12 (N=12, M=3, closed)"),
@@ -39,8 +42,8 @@ CONFIGS = {
 }
 
 
-# GOPs per GPU per step (c5: I-only, one picture per "GOP"; c4: 4K, 192 frames = 2.4 GB per step)
-DEFAULT_GOPS = {"c2": 64, "c3": 64, "c4": 16, "c5": 64}
+# GOPs per GPU per step (c1, c5: I-only, one picture per "GOP"; c4: 4K, 192 frames = 2.4 GB per step)
+DEFAULT_GOPS = {"c1": 120, "c2": 64, "c3": 64, "c4": 16, "c5": 64}
 
 
 def algorithmic_bytes(parsed):
@@ -355,6 +358,7 @@ def main():
                      "dominant_kernel": dominant, "one_stream_span_ms": round(span1, 4),
                      "per_kernel": per_kernel},
         "frame_digest_of_digests": int(np.bitwise_xor.reduce(np.concatenate(gathered))),
+        "provenance": _build.provenance(),
     }
     if gather_res is not None:
         result["frame_gather"] = gather_res

@@ -198,16 +198,17 @@ def test_back_to_back_batches_and_their_timing_events():
         assert span > 0 and launches and all(t > 0 for t in launches)
 
 
-@pytest.mark.parametrize("config", ["c3", "c4", "c5"])
+@pytest.mark.parametrize("config", ["c1", "c3", "c4", "c5"])
 def test_bench_config_full_size_every_frame_vs_oracle(config):
-    """The other bench configurations at full size (SURVEY §8d C3 1080p 4:2:2 IPB, C4 4K 4:2:0
-    IPB, C5 1080p 4:4:4 I-only high bitrate): one closed GOP (C5: 4 I pictures) generated exactly
+    """The other bench configurations at full size (SURVEY §8d C1 1080p 4:2:0 I-only, C3 1080p
+    4:2:2 IPB, C4 4K 4:2:0 IPB, C5 1080p 4:4:4 I-only high bitrate): one closed GOP (C1/C5: 4 I
+    pictures) generated exactly
     as bench.py generates it, every frame's device digest == the digest of the oracle's frame,
     and the first and last frames compared byte for byte."""
     import importlib
     bench = importlib.import_module("bench")
     width, height, cf, gparams, _ = bench.CONFIGS[config]
-    es = R.generate_es(width=width, height=height, chroma_format=cf, n_gops=4 if config == "c5" else 1,
+    es = R.generate_es(width=width, height=height, chroma_format=cf, n_gops=4 if config in ("c1", "c5") else 1,
                        seed=1729, **gparams)
     parsed = R.Parsed(es, width, height, cf)
     exp = oracle_frames(parsed)

@@ -76,8 +76,46 @@ def _compile(src, obj, stamp):
     return obj
 
 
+def _git_head():
+    """`git rev-parse HEAD` (+ "-dirty" when tracked files differ), or None without a checkout."""
+    try:
+        head = subprocess.run(["git", "-C", REPO, "rev-parse", "HEAD"], capture_output=True, text=True,
+                              timeout=20).stdout.strip()
+        if not head:
+            return None
+        dirty = subprocess.run(["git", "-C", REPO, "status", "--porcelain", "--untracked-files=no"],
+                               capture_output=True, text=True, timeout=20).stdout.strip()
+        return head + ("-dirty" if dirty else "")
+    except (OSError, subprocess.SubprocessError):
+        return None
+
+
+def provenance():
+    """What a log or bench line ran: the git commit (live in a checkout; on the GPU box, which gets
+    the tree without .git, the commit build() recorded in _build/HEAD) and the library's content
+    stamp (a SHA-256 over every source, header and build command: recomputable from any commit)."""
+    head = _git_head()
+    src = "git"
+    if head is None:
+        try:
+            with open(os.path.join(OUT, "HEAD")) as fh:
+                head, src = fh.read().strip() or None, "_build/HEAD (recorded by build())"
+        except OSError:
+            src = None
+    try:
+        with open(LIB + ".stamp") as fh:
+            stamp = fh.read().strip()
+    except OSError:
+        stamp = None
+    return {"head": head, "head_source": src, "libmp2vg_stamp": stamp}
+
+
 def build(verbose=False):
     os.makedirs(OUT, exist_ok=True)
+    head = _git_head()
+    if head is not None:
+        with open(os.path.join(OUT, "HEAD"), "w") as fh:
+            fh.write(head + "\n")
     srcs = sorted(glob.glob(os.path.join(CSRC, "*.cpp")) + glob.glob(os.path.join(CSRC, "*.hip")))
     hdrs = _headers()
     objs = [os.path.join(OUT, os.path.basename(s) + ".o") for s in srcs]
