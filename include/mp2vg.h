@@ -36,7 +36,9 @@
 extern "C" {
 #endif
 
-#define MP2VG_ABI_VERSION 1
+/* 2: coefficient words carry the MB column mod 8 in bits 26-28 and the FIRST1S / DC flags in
+ *    bits 29 / 30 (1: FIRST1S bit 26, DC bit 27, MB column bits 28-30); mp2vg_frame_t.device */
+#define MP2VG_ABI_VERSION 2
 
 /* ---- status codes --------------------------------------------------------------------- */
 enum {
@@ -323,7 +325,9 @@ typedef struct mp2vg_decoder mp2vg_decoder_t;
 int  mp2vg_decoder_create(const mp2vg_config_t* cfg, mp2vg_render_fn fn, void* user,
                           mp2vg_decoder_t** out);
 /* The drop-in decoder over several devices (GOP sharding): the independent shards of a stream
- * (mp2vg_parsed_shards) are dealt round-robin, shard s -> devices[s % ndevices], each device
+ * (mp2vg_parsed_shards) are merged in decode order into runs of at least one decode chunk (16
+ * pictures: consecutive shards join a run until it is that long) and the runs are dealt
+ * round-robin, run r -> devices[r % ndevices], each device
  * decoding its shards with its own frame pool, record banks and streams, concurrently; frames
  * reach the renderer in the stream's display order whatever device decoded them.  cfg->device is
  * ignored; a device may be listed more than once (e.g. {0, 0}: two independent lanes on one GPU).

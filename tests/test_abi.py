@@ -40,7 +40,7 @@ def test_library_is_gfx950_code_object():
 
 def test_abi_version_and_status_strings():
     L = _lib.lib()
-    assert L.mp2vg_abi_version() == 1
+    assert L.mp2vg_abi_version() == 2  # 2: coefficient-word bit layout of round 2
     for s in (0, -1, -2, -3, -4, -5, -6):
         assert L.mp2vg_status_string(s)
 

@@ -160,15 +160,45 @@ def test_dropin_gop_sharding_over_device_lanes(devices):
     lanes = dec.lane_frames()
     dec.close()
     assert got == exp and order == list(parsed.display)
+    # shards merge into runs of >= 16 pictures (two 12-picture GOPs each, the last GOP alone) and
+    # run r goes to lane r % n
     n = len(devices)
-    assert lanes == [12 * len(range(i, 7, n)) for i in range(n)]
+    runs = [24, 24, 24, 12]
+    assert lanes == [sum(runs[r] for r in range(i, len(runs), n)) for i in range(n)]
+
+
+def test_dropin_lanes_long_gops_bounded_pool_and_i_only():
+    """Two lanes on long closed GOPs (96 pictures, longer than the 72-frame pool) keep the frame pool
+    at its reserved size -- a lane's last chunk completes when the stream moves to the other lane,
+    so display order never waits on an idle lane -- and an I-only stream (one shard per picture)
+    is dealt in whole runs, both lanes used, frames in display order and oracle-exact."""
+    from tiny_mp2v_dec_amd.records import generate_es
+    for kw, nshards in ((dict(n_gops=3, gop_n=96, gop_m=3), 3), (dict(n_gops=40, gop_n=1, gop_m=1, mix=1), 40)):
+        es = generate_es(width=176, height=144, chroma_format=1, seed=65, **kw)
+        exp, parsed = _oracle_md5(es, 176, 144, 1)
+        assert parsed.nshards == nshards
+        got = []
+        dec = mp2v_decoder_c(decoder_config_t(176, 144, 1, num_threads=4, devices=[0, 0]),
+                             lambda f: got.append(hashlib.md5(f.yuv_bytes()).hexdigest()))
+        before = dec.frames_allocated()
+        dec.decode(es)
+        after = dec.frames_allocated()
+        lanes = dec.lane_frames()
+        dec.close()
+        assert got == exp
+        assert after == before, (kw, before, after)
+        assert all(n > 0 for n in lanes) and sum(lanes) == parsed.npics
+        if nshards == 40:  # runs of 16, 16, 8 pictures
+            assert lanes == [24, 16]
 
 
 def test_dropin_gop_sharding_golden_and_open_gop():
-    """Golden streams through two lanes: the closed-GOP stream splits over both lanes, the open-GOP
-    stream is one shard (its B pictures predict across the GOP) and stays on lane 0; both give
-    the reference's MD5s."""
-    for name, split in (("ipb420_qcif", True), ("ipb420_qcif_openb", False)):
+    """Golden streams through two lanes give the reference's MD5s: the closed-GOP stream is two
+    12-picture shards, which merge into one run (runs are at least a 16-picture chunk), and the
+    open-GOP stream is one shard (its B pictures predict across the GOP); both stay on lane 0
+    (streams that do split over lanes: test_dropin_gop_sharding_over_device_lanes)."""
+    from tiny_mp2v_dec_amd.records import Parsed
+    for name, nshards in (("ipb420_qcif", 2), ("ipb420_qcif_openb", 1)):
         e = next(m for m in MANIFEST if m["name"] == name)
         es = read_stream(e)
         got = []
@@ -178,7 +208,8 @@ def test_dropin_gop_sharding_golden_and_open_gop():
         lanes = dec.lane_frames()
         dec.close()
         assert got == e["md5"], name
-        assert (lanes[1] > 0) == split, (name, lanes)
+        assert Parsed(es, e["width"], e["height"], e["chroma_format"]).nshards == nshards
+        assert lanes == [len(e["md5"]), 0], (name, lanes)
 
 
 def test_dropin_gop_sharding_device_frames():

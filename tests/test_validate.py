@@ -98,3 +98,29 @@ def test_coefficient_array_limit():
                                          mode.ctypes.data_as(i32p), len(mode))
     assert rc == -1  # MP2VG_E_INVALID
     assert "coefficient words" in _lib.lib().mp2vg_last_error().decode()
+
+
+@pytest.mark.parametrize("cf", [1, 2, 3])
+def test_motion_vectors_outside_the_reference_rejected(cf):
+    """Every vector the kernel applies must keep its reads inside the reference planes, the input
+    contract the reference itself relies on (mb_decoder.cpp:212-289; the kernel's row offsets are
+    not clamped into the plane): a forward or backward vector one half-pel past the left, top,
+    right or bottom edge is refused, the vector at the edge is not."""
+    p = _parsed(cf, fpfd=0)
+    w, h = p.width, p.height
+    fl = p.mbs["flags"].astype(np.int64)
+    inter = np.nonzero(((fl & _lib.MB_INTRA) == 0) & ((fl & 8) == 0))[0]  # frame-MC inter MBs
+    k = int(inter[0])
+    s = 1 if (fl[k] & 4) and not (fl[k] & 2) else 0  # a direction this MB uses
+    x, y = int(p.mbs["x"][k]), int(p.mbs["y"][k])
+    R.validate_batch(w, h, cf, p.npics, p.pics, p.mbs, p.coefs)
+    for mvx, mvy, ok in ((-2 * 16 * x, 0, True), (-2 * 16 * x - 1, 0, False), (0, -2 * 16 * y, True),
+                         (0, -2 * 16 * y - 2, False), (2 * (w - 16 - 16 * x), 0, True),
+                         (2 * (w - 16 - 16 * x) + 1, 0, False), (0, 2 * (h - 16 - 16 * y) + 2, False)):
+        mbs = p.mbs.copy()
+        mbs["mv"][k, 0, s] = (mvx, mvy)
+        if ok:
+            R.validate_batch(w, h, cf, p.npics, p.pics, mbs, p.coefs)
+        else:
+            with pytest.raises(_lib.Mp2vgError, match="reads outside the reference"):
+                R.validate_batch(w, h, cf, p.npics, p.pics, mbs, p.coefs)

@@ -329,7 +329,20 @@ extern "C" int mp2vg_decoder_decode(mp2vg_decoder_t* d, const uint8_t* buf, uint
     std::vector<int32_t> display(parse_session_display(ps), parse_session_display(ps) + npics);
     const int32_t* shard = parse_session_shards(ps);
     const int nl = (int)d->lanes.size();
-    auto lane_of = [&](int p) -> Lane& { return *d->lanes[shard[p] % nl]; };
+    // Lanes take runs of whole shards, each run at least a chunk long: consecutive shards merge
+    // until the run holds kChunk pictures, and run r goes to lane r % nl.  An I-only stream (one
+    // shard per picture) then still feeds each lane full chunks instead of alternating lanes
+    // picture by picture (one upload, launch chain and download sync per picture).
+    std::vector<int32_t> lane_idx(npics, 0);
+    for (int p = 0, run = 0, len = 0; p < npics; p++) {
+        if (p > 0 && shard[p] != shard[p - 1] && len >= kChunk) {
+            run++;
+            len = 0;
+        }
+        lane_idx[p] = run % nl;
+        len++;
+    }
+    auto lane_of = [&](int p) -> Lane& { return *d->lanes[lane_idx[p]]; };
 
     // a reference on another lane: the forward anchor of a closed GOP's leading B picture, which
     // its macroblocks never read (mp2vg_parsed_shards); checked on its records below
@@ -555,11 +568,17 @@ extern "C" int mp2vg_decoder_decode(mp2vg_decoder_t* d, const uint8_t* buf, uint
     // chunks: up to kChunk consecutive pictures of one lane; with several lanes a chunk also ends
     // where the stream moves to the next shard's lane, so the chunks (and the parse window) still
     // advance in decode order and every lane decodes while the next one is being fed
+    Lane* prev = nullptr;
     for (int s = 0; s < npics;) {
         Lane& L = lane_of(s);
         int e = s + 1;
         while (e < npics && e - s < kChunk && (nl == 1 || &lane_of(e) == &L)) e++;
         if ((rc = run_chunk(L, s, e)) != MP2VG_OK) return finish(rc);
+        // the lane just left finishes its last chunk now (this lane's chunk is already queued):
+        // otherwise its frames wait in flight until it runs again, display order stalls behind
+        // them, and the renderer idles while the frame pool grows
+        if (prev && prev != &L && (rc = complete_pending(*prev)) != MP2VG_OK) return finish(rc);
+        prev = &L;
         s = e;
     }
     for (auto& Lp : d->lanes)

@@ -336,10 +336,12 @@ __device__ __forceinline__ void tap_issue(Tap<NW>& t, bool use, __amdgpu_buffer_
         Y = mby_base + fs + 2 * ((py >> 1) + (mvy >> 1));
         step = 2;
     }
-    // clamp into the plane so out-of-contract vectors can never fault (inactive in contract)
-    const int Xc = min(max(X, 0), stride - 4);
-    const int Y0 = min(max(Y, 0), ph - 1);
-    const int Y1 = min(max(Y + step, 0), ph - 1);
+    // no clamp into the plane: mp2vg_batch_upload refuses any vector whose reads leave the
+    // reference planes (the reference's own input contract), and a row offset out of the slot
+    // still cannot fault -- the buffer resource returns 0 past num_records
+    const int Xc = X;
+    const int Y0 = Y;
+    const int Y1 = Y + step;
     const int hx = mvx & 1, hy = mvy & 1;
     const bool edge = py + step >= phm;
     t.ctl = (uint32_t)((Xc & 3) | (hx << 2) | (hy << 3) | ((int)use << 4) | ((int)edge << 5) | ((int)field << 6));
@@ -788,16 +790,23 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, LT&
             // words past the prefetch: XW loads per lane in flight per round trip, not one (a 4:4:4
             // intra group carries ~1,400 words)
             constexpr int XW = MCM == 0 ? 8 : 2;
-            for (int base = 64 * NCW; base < S.ncoef; base += 64 * XW) {
-                uint32_t xw[XW];
+            if (S.ncoef > 64 * NCW) {
+                for (int base = 64 * NCW; base < S.ncoef; base += 64 * XW) {
+                    uint32_t xw[XW];
 #pragma unroll
-                for (int j = 0; j < XW; j++) {
-                    const int wi = base + 64 * j + lane;
-                    xw[j] = wi < S.ncoef ? c.coefs[S.coef0 + wi] : 0u;
+                    for (int j = 0; j < XW; j++) {
+                        const int wi = base + 64 * j + lane;
+                        xw[j] = wi < S.ncoef ? c.coefs[S.coef0 + wi] : 0u;
+                    }
+#pragma unroll
+                    for (int j = 0; j < XW; j++)
+                        if (base + 64 * j + lane < S.ncoef) dequant_word<LT, MCM == 0>(L, wave, xw[j]);
                 }
-#pragma unroll
-                for (int j = 0; j < XW; j++)
-                    if (base + 64 * j + lane < S.ncoef) dequant_word<LT, MCM == 0>(L, wave, xw[j]);
+                // Drain this rare path's loads before it rejoins: the waitcnt pass merges the
+                // paths' pending-load state, and a load it cannot prove retired (a lane-masked
+                // one) made it put a vmcnt(0) -- every tap of g+1 and the previous stores in
+                // flight -- on the common path, once per group.
+                __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0) expcnt(7) lgkmcnt(15)
             }
         }
         // first 64*NCW coefficient words of g+1 (the words of g are consumed)

@@ -90,7 +90,10 @@ struct mp2vg_ctx {
     // timing events of the last kHist batches (ring, slot = batch sequence number % kHist), so a
     // caller can decode back to back and read every batch's times afterwards
     struct BatchEv {
-        hipEvent_t b[2] = {nullptr, nullptr};  // whole batch, main stream
+        hipEvent_t b[2] = {nullptr, nullptr};  // b[1]: end of the whole batch (main stream)
+        std::vector<hipEvent_t> s;             // start of each picture set (on its stream; the
+                                               // batch starts at the earliest of them)
+        int ns = 0;                            // sets of this batch
         std::vector<hipEvent_t> l;             // 2 per launch (start, end; on the launch's stream)
         int nl = 0;                            // launches timed (0 with launch timing off)
     };
@@ -301,8 +304,18 @@ static int plan_batch(mp2vg_ctx_t* c, const mp2vg_picture_t* pics, int32_t npics
                 return "intra macroblock whose cbp does not code every block";
             if (P.picture_coding_type == 1 && !(m.flags & MP2VG_MB_INTRA)) return "non-intra macroblock in an I picture";
             if (!(m.flags & MP2VG_MB_INTRA)) {
-                uses[0] |= (m.flags & MP2VG_MB_FWD) || !(m.flags & MP2VG_MB_BWD);
-                uses[1] |= (m.flags & MP2VG_MB_BWD) != 0;
+                const bool dir[2] = {(m.flags & MP2VG_MB_FWD) || !(m.flags & MP2VG_MB_BWD), (m.flags & MP2VG_MB_BWD) != 0};
+                uses[0] |= dir[0];
+                uses[1] |= dir[1];
+                // every vector the kernel applies reads inside the reference planes (the input
+                // contract the reference relies on, mb_decoder.cpp:212-289): the kernel's row
+                // offsets are not clamped into the plane
+                const bool field = m.flags & MP2VG_MB_FIELD_MC;
+                for (int r = 0; r < (field ? 2 : 1); r++)
+                    for (int s = 0; s < 2; s++)
+                        if (dir[s] && !mc_reads_inside(c->g, m.x, m.y, m.mv[r][s][0], m.mv[r][s][1], field,
+                                                       (m.flags & MP2VG_MB_FS_BIT(r, s)) ? 1 : 0, r))
+                            return "motion vector reads outside the reference planes";
             }
         }
         uses_of[2 * (size_t)p] = uses[0];
@@ -581,7 +594,15 @@ extern "C" int mp2vg_batch_decode(mp2vg_ctx_t* c) {
             if (overlap) HIPCHK(hipStreamWaitEvent(st, c->sev[t], 0));
         }
     }
-    HIPCHK(hipEventRecord(H.b[0], stream_of(0)));
+    // every set's start (after its waits): a set with no overlap with the previous batch starts
+    // before set 0 does, so one start event on set 0 would under-report the batch span
+    while ((int)H.s.size() < nsets) {
+        hipEvent_t e;
+        HIPCHK(hipEventCreate(&e));
+        H.s.push_back(e);
+    }
+    for (int set = 0; set < nsets; set++) HIPCHK(hipEventRecord(H.s[set], stream_of(set)));
+    H.ns = nsets;
     for (int i = 0; i < nl; i++) {
         const hipStream_t st = stream_of(launches[i].set);
         a.slice_base = launches[i].begin;
@@ -612,6 +633,19 @@ extern "C" int mp2vg_synchronize(mp2vg_ctx_t* c) {
     return MP2VG_OK;
 }
 
+// time from the earliest set start of batch H to event end
+static hipError_t since_earliest_start(const mp2vg_ctx::BatchEv& H, hipEvent_t end, float* ms) {
+    float best = 0;
+    for (int i = 0; i < H.ns; i++) {
+        float t;
+        hipError_t e = hipEventElapsedTime(&t, H.s[i], end);
+        if (e != hipSuccess) return e;
+        best = i == 0 ? t : std::max(best, t);
+    }
+    *ms = best;
+    return hipSuccess;
+}
+
 extern "C" int mp2vg_batch_times(mp2vg_ctx_t* c, int32_t back, float* batch_ms, float* launch_ms, int32_t max,
                                  int32_t* count) {
     if (!c || back < 0) return MP2VG_E_INVALID;
@@ -622,7 +656,7 @@ extern "C" int mp2vg_batch_times(mp2vg_ctx_t* c, int32_t back, float* batch_ms, 
     HIPCHK(hipSetDevice(c->cfg.device));
     HIPCHK(hipStreamSynchronize(c->stream));
     const mp2vg_ctx::BatchEv& H = c->hist[(c->seq - 1 - (uint64_t)back) % mp2vg_ctx::kHist];
-    if (batch_ms) HIPCHK(hipEventElapsedTime(batch_ms, H.b[0], H.b[1]));
+    if (batch_ms) HIPCHK(since_earliest_start(H, H.b[1], batch_ms));
     if (count) *count = H.nl;
     for (int i = 0; launch_ms && i < H.nl && i < max; i++)
         HIPCHK(hipEventElapsedTime(&launch_ms[i], H.l[2 * i], H.l[2 * i + 1]));
@@ -639,7 +673,7 @@ extern "C" int mp2vg_batches_span(mp2vg_ctx_t* c, int32_t back_first, int32_t ba
     HIPCHK(hipStreamSynchronize(c->stream));
     const mp2vg_ctx::BatchEv& A = c->hist[(c->seq - 1 - (uint64_t)back_first) % mp2vg_ctx::kHist];
     const mp2vg_ctx::BatchEv& B = c->hist[(c->seq - 1 - (uint64_t)back_last) % mp2vg_ctx::kHist];
-    HIPCHK(hipEventElapsedTime(ms, A.b[0], B.b[1]));
+    HIPCHK(since_earliest_start(A, B.b[1], ms));
     return MP2VG_OK;
 }
 

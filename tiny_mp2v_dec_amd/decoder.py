@@ -11,7 +11,8 @@ frame_c layout before the renderer runs.  A frame is valid only during the callb
 frame pool recycling, threads.cpp:75-80); copy it to keep it.
 
 decoder_config_t(devices=[0, 1, ...]) shards the stream by GOP over several GPUs
-(mp2vg_decoder_create_multi: independent shard s -> devices[s % len(devices)]); frames still reach
+(mp2vg_decoder_create_multi: independent shards merged into runs of >= 16 pictures, run r ->
+devices[r % len(devices)]); frames still reach
 the renderer in display order.  After decode(), m_sequence_header / m_sequence_extension /
 m_sequence_display_extension / m_group_of_pictures_header hold the stream's headers as the
 reference's public members do (decoder.h:124-130).
