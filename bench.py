@@ -349,6 +349,13 @@ def main():
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic["traffic_bytes_per_step"] if traffic else None,
                      "traffic_unit": "bytes/step (HBM, PMC)", "traffic_source": traffic["source"] if traffic else None,
+                     "traffic_fetch_raw": traffic.get("fetch_raw_bytes_per_step") if traffic else None,
+                     "traffic_write": traffic.get("write_bytes_per_step") if traffic else None,
+                     "l2_requests_per_step": traffic.get("l2_requests_per_step") if traffic else None,
+                     "l2_hit_rate": traffic.get("l2_hit_rate") if traffic else None,
+                     # on-chip bound: L1->L2 request bytes (64 B per request) over the algorithmic bytes
+                     "l1l2_amplification": (round(traffic["l2_requests_per_step"] * 64 / alg_bytes, 3)
+                                            if traffic and traffic.get("l2_requests_per_step") else None),
                      "kernel": "mp2vg::recon_kernel", "launches_per_step": len(kernel_ms[0]),
                      "avg_launch_ms": round(float(np.mean(per_launch)), 4),
                      "algorithmic_bytes_per_step": int(alg_bytes), "bytes_breakdown": parts,

@@ -82,15 +82,30 @@ def main():
             wsum = sum(counters["WRITE_SIZE"]) * 1024 / args.steps_total
             lines.append(f"per bench step ({args.steps_total} steps profiled): FETCH x2 {fsum / 1e9:.3f} GB + WRITE "
                          f"{wsum / 1e9:.3f} GB = {(fsum + wsum) / 1e9:.3f} GB")
+            reqs = None
+            if "TCC_HIT_sum" in counters and "TCC_MISS_sum" in counters:
+                hit = sum(counters["TCC_HIT_sum"]) / args.steps_total
+                miss = sum(counters["TCC_MISS_sum"]) / args.steps_total
+                reqs = hit + miss
+                lines.append(f"L2 (TCC) requests per bench step: {reqs / 1e6:.1f} M (hit rate {hit / reqs:.3f})")
             if args.json:
                 import json
+                out = {"tag": args.tag, "config": args.config, "gops": args.gops,
+                       "traffic_bytes_per_step": int(fsum + wsum), "fetch_x2_bytes_per_step": int(fsum),
+                       "fetch_raw_bytes_per_step": int(fsum / 2), "write_bytes_per_step": int(wsum),
+                       "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes (KiB), summed over the "
+                                 "recon_kernel dispatches of the profiled bench run / steps. FETCH_SIZE = 64 B per "
+                                 "L2-to-fabric read request (tools/fetch_calib.hip: a coalesced 128-B line is one "
+                                 "request, and so is a 20-B tap row on one missed line), so raw FETCH is the lower "
+                                 "bound of the bytes read and FETCH x2 (128 B per request, the gfx950 correction of "
+                                 "MI355X_MICROARCH.md) the upper; traffic = FETCH x2 + WRITE (WRITE_SIZE is exact "
+                                 "for the kernel's 64-B and 128-B row stores)"}
+                if reqs is not None:
+                    out.update({"l2_requests_per_step": int(reqs), "l2_hit_rate": round(hit / reqs, 4),
+                                "l2_request_method": "TCC_HIT_sum + TCC_MISS_sum (one request per 128-B line an "
+                                                     "L1 miss touches, tools/fetch_calib.hip)"})
                 with open(args.json, "w") as fh:
-                    json.dump({"tag": args.tag, "config": args.config, "gops": args.gops,
-                               "traffic_bytes_per_step": int(fsum + wsum), "fetch_x2_bytes_per_step": int(fsum),
-                               "write_bytes_per_step": int(wsum),
-                               "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes (KiB), "
-                                         "FETCH x2 (gfx950 wide-read correction, MI355X_MICROARCH.md), summed over "
-                                         "the recon_kernel dispatches of the profiled bench run / steps"}, fh, indent=1)
+                    json.dump(out, fh, indent=1)
         lines.append("")
     text = "\n".join(lines)
     print(text)
