@@ -146,6 +146,101 @@ def profiled_traffic(config, gops):
     return d
 
 
+def init_distributed(backend):
+    """One process per GPU (torch.distributed.run env).  nccl (= RCCL on ROCm): the rank's GPU is
+    set first and the process group is bound to it (device_id: eager communicator init), and the
+    collectives move cuda tensors; gloo: CPU tensors (several ranks may share one GPU).
+    Returns (rank, world, dist or None, collective device, local GPU index)."""
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    ndev = max(1, torch.cuda.device_count())  # does not initialise the GPU
+    device = local_rank % ndev
+    dist, coll_dev = None, "cpu"
+    if world > 1:
+        import torch.distributed as tdist
+        if backend == "nccl":
+            torch.cuda.set_device(device)
+            tdist.init_process_group("nccl", device_id=torch.device("cuda", device))
+            coll_dev = f"cuda:{device}"
+        else:
+            tdist.init_process_group("gloo")
+        dist = tdist
+    return rank, world, dist, coll_dev, device
+
+
+def parity_over_ranks(dig, exp, dist, coll_dev):
+    """Every rank's frame digests vs the compiled reference's (exp, or None when the workload has
+    none), gathered to all ranks.  Returns (parity record, per-rank digest arrays)."""
+    from tiny_mp2v_dec_amd import gather as G
+    my_status = 2 if exp is None else (1 if np.array_equal(dig, exp) else 0)  # 2 unchecked, 1 ok, 0 bad
+    gathered = G.gather_u64(dig, dist, coll_dev)
+    statuses = [int(x[0]) for x in G.gather_u64(np.array([my_status], np.uint64), dist, coll_dev)]
+    if any(s == 0 for s in statuses):
+        parity = {"status": "MISMATCH", "ranks_mismatching": [r for r, s in enumerate(statuses) if s == 0]}
+    elif all(s == 1 for s in statuses):
+        parity = {"status": "bit-exact", "frames_checked": int(sum(len(g) for g in gathered)),
+                  "against": "tests/golden/bench_digests.npz: per-frame digests of the compiled reference "
+                             "decoder (1 thread) on each rank's stream"}
+    else:
+        parity = {"status": "unchecked", "why": "no reference digests for this workload/seed in "
+                                                "tests/golden/bench_digests.npz"}
+    return parity, gathered
+
+
+def frame_gather(dist, coll_dev, parsed, fb, copy_frame, pw, ph, gathered, gather_gops):
+    """The rank-0 frame gather of the first `gather_gops` GOPs of every rank (GOP g of the virtual
+    stream = GOP g // world of rank g % world), display order, timed with max over ranks; rank 0
+    spot-checks the first and last frame of two GOPs per rank against that rank's digests.
+    copy_frame(decode index, uint8 tensor on coll_dev, on_device) packs a decoded frame."""
+    import torch
+    from tiny_mp2v_dec_amd import gather as G
+    rank, world = dist.get_rank(), dist.get_world_size()
+    ng = min(gather_gops, int(parsed.gop.max()) + 1)
+    on_dev = coll_dev != "cpu"
+    gop_sizes, gop_frames = [], {}
+    for g in range(ng * world):
+        local = [int(d) for d in parsed.display if parsed.gop[d] == g // world]
+        gop_sizes.append(len(local))
+        if g % world == rank:
+            fr = []
+            for d in local:
+                t = torch.empty(fb, dtype=torch.uint8, device=coll_dev)
+                copy_frame(d, t, on_dev)
+                fr.append(t)
+            gop_frames[g] = fr
+    if on_dev:
+        torch.cuda.synchronize()
+    dist.barrier()
+    tg = time.perf_counter()
+    got = G.gather_gops(dist, gop_frames, gop_sizes, fb, device=coll_dev)
+    if on_dev:
+        torch.cuda.synchronize()
+    tg = G.max_over_ranks(time.perf_counter() - tg, dist, coll_dev)
+    res = None
+    if rank == 0:
+        # every rank's stream has the same GOP structure, so rank 0's own display order and GOP
+        # index map a gathered position to the sender's decode index
+        starts = np.concatenate([[0], np.cumsum(gop_sizes)])
+        ok = True
+        for r in range(min(world, ng * world)):
+            for g in (r, r + world * (ng - 1)):
+                local = [int(d) for d in parsed.display if parsed.gop[d] == g // world]
+                for k in (0, len(local) - 1):
+                    buf = got[int(starts[g]) + k].cpu().numpy()
+                    planes, o = [], 0
+                    for i in range(3):
+                        planes.append(buf[o:o + pw[i] * ph[i]].reshape(ph[i], pw[i]))
+                        o += pw[i] * ph[i]
+                    ok &= R.planes_digest(planes) == int(gathered[r][local[k]])
+        res = {"frames": len(got), "bytes": int(len(got) * fb), "ms": round(tg * 1e3, 3),
+               "GBps_into_rank0": round(len(got) * fb / tg / 1e9, 2), "verified": bool(ok),
+               "sample": f"first {ng} GOPs of every rank, frame by frame in display order"}
+    del gop_frames, got
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -162,23 +257,8 @@ def main():
     ap.add_argument("--no-e2e", action="store_true", help="skip the drop-in end-to-end measurement")
     args = ap.parse_args()
 
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    coll_dev = "cpu"
+    rank, world, dist, coll_dev, device = init_distributed(args.backend)
     import torch
-    ndev = max(1, torch.cuda.device_count())  # does not initialise the GPU
-    device = local_rank % ndev
-    if world > 1:
-        import torch.distributed as tdist
-        if args.backend == "nccl":
-            torch.cuda.set_device(device)
-            tdist.init_process_group("nccl", device_id=torch.device("cuda", device))
-            coll_dev = f"cuda:{device}"
-        else:
-            tdist.init_process_group("gloo")
-        dist = tdist
 
     if rank == 0:
         _build.build()
@@ -230,18 +310,7 @@ def main():
     # ---- parity of the timed batch: device digest of every frame vs the compiled reference's ----
     dig = ctx.digests(np.arange(parsed.npics))
     exp = expected_digests(args.config, gops, seed)
-    my_status = 2 if exp is None else (1 if np.array_equal(dig, exp) else 0)  # 2 unchecked, 1 ok, 0 bad
-    gathered = G.gather_u64(dig, dist, coll_dev)
-    statuses = [int(x[0]) for x in G.gather_u64(np.array([my_status], np.uint64), dist, coll_dev)]
-    if any(s == 0 for s in statuses):
-        parity = {"status": "MISMATCH", "ranks_mismatching": [r for r, s in enumerate(statuses) if s == 0]}
-    elif all(s == 1 for s in statuses):
-        parity = {"status": "bit-exact", "frames_checked": int(sum(len(g) for g in gathered)),
-                  "against": "tests/golden/bench_digests.npz: per-frame digests of the compiled reference "
-                             "decoder (1 thread) on each rank's stream"}
-    else:
-        parity = {"status": "unchecked", "why": "no reference digests for this workload/seed in "
-                                                "tests/golden/bench_digests.npz"}
+    parity, gathered = parity_over_ranks(dig, exp, dist, coll_dev)
 
     # ---- per-kernel roofline: the same batch on a one-stream context, so launches never overlap ----
     of_pic, modes = R.plan_batch(width, height, cf, parsed.npics, parsed.pics, parsed.mbs, parsed.coefs,
@@ -276,49 +345,9 @@ def main():
     # ---- rank-0 frame gather (grouped send/recv per round of GOPs, display order), timed apart ----
     gather_res = None
     if dist is not None:
-        ng = min(args.gather_gops, int(parsed.gop.max()) + 1)
-        fb = ctx.frame_bytes()
-        on_dev = coll_dev != "cpu"
-        gop_sizes, gop_frames = [], {}
-        for g in range(ng * world):  # virtual stream: GOP g = GOP g // world of rank g % world
-            local = [int(d) for d in parsed.display if parsed.gop[d] == g // world]
-            gop_sizes.append(len(local))
-            if g % world == rank:
-                fr = []
-                for d in local:
-                    t = torch.empty(fb, dtype=torch.uint8, device=coll_dev)
-                    ctx.copy_packed(d, t.data_ptr(), on_dev)
-                    fr.append(t)
-                gop_frames[g] = fr
-        if on_dev:
-            torch.cuda.synchronize()
-        barrier()
-        tg = time.perf_counter()
-        got = G.gather_gops(dist, gop_frames, gop_sizes, fb, device=coll_dev)
-        if on_dev:
-            torch.cuda.synchronize()
-        tg = G.max_over_ranks(time.perf_counter() - tg, dist, coll_dev)
-        if rank == 0:
-            # spot-check: the first and last gathered frame of every rank == that rank's device digest
-            # of the same picture (every rank's stream has the same GOP structure, so rank 0's own
-            # display order and GOP index map a gathered position to the sender's decode index)
-            pw, ph = ctx.pw, ctx.ph
-            starts = np.concatenate([[0], np.cumsum(gop_sizes)])
-            ok = True
-            for r in range(min(world, ng * world)):
-                for g in (r, r + world * (ng - 1)):
-                    local = [int(d) for d in parsed.display if parsed.gop[d] == g // world]
-                    for k in (0, len(local) - 1):
-                        buf = got[int(starts[g]) + k].cpu().numpy()
-                        planes, o = [], 0
-                        for i in range(3):
-                            planes.append(buf[o:o + pw[i] * ph[i]].reshape(ph[i], pw[i]))
-                            o += pw[i] * ph[i]
-                        ok &= R.planes_digest(planes) == int(gathered[r][local[k]])
-            gather_res = {"frames": len(got), "bytes": int(len(got) * fb), "ms": round(tg * 1e3, 3),
-                          "GBps_into_rank0": round(len(got) * fb / tg / 1e9, 2), "verified": bool(ok),
-                          "sample": f"first {ng} GOPs of every rank, frame by frame in display order"}
-        del gop_frames, got
+        gather_res = frame_gather(dist, coll_dev, parsed, ctx.frame_bytes(),
+                                  lambda d, t, on_dev: ctx.copy_packed(d, t.data_ptr(), on_dev),
+                                  ctx.pw, ctx.ph, gathered, args.gather_gops)
 
     traffic = profiled_traffic(args.config, gops)
     frames_total = parsed.npics * world * args.steps

@@ -172,3 +172,111 @@ def test_rank0_frame_gather_display_order(world):
     assert got == [frame_yuv_bytes(fr[d]) for d in full.display]
     assert mx == float(world)
     assert u == [[(1 << 63) + k for k in range(r + 2)] for r in range(world)]
+
+
+def _bench_phase_worker(rank, world, port, q, bad_rank):
+    """bench.py's distributed phases -- init_distributed (the torch.distributed.run environment),
+    parity_over_ranks and frame_gather -- exactly as bench.py calls them at N > 1, with the oracle
+    standing in for the kernel: each rank decodes its own stream (seed 1729 + rank)."""
+    import sys
+    sys.path[:0] = [REPO, os.path.join(REPO, "tests")]
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    import torch
+    import bench
+    from helpers import oracle_frames
+    from tiny_mp2v_dec_amd.records import Parsed, frame_yuv_bytes, generate_es, planes_digest
+
+    r, w, d, coll_dev, device = bench.init_distributed("gloo")
+    assert (r, w, coll_dev, device) == (rank, world, "cpu", 0) and d is not None
+    es = generate_es(width=176, height=144, chroma_format=1, n_gops=3, gop_n=6, gop_m=3, seed=1729 + rank)
+    parsed = Parsed(es, 176, 144, 1)
+    frames = oracle_frames(parsed)
+    dig = np.array([planes_digest(f) for f in frames], np.uint64)
+    exp = dig.copy()
+    if rank == bad_rank:
+        exp[1] ^= np.uint64(1)
+    parity, gathered = bench.parity_over_ranks(dig, exp, d, coll_dev)
+
+    def copy_frame(i, t, on_dev):
+        assert not on_dev and t.device == torch.device(coll_dev)
+        t.copy_(torch.from_numpy(np.frombuffer(frame_yuv_bytes(frames[i]), np.uint8).copy()))
+
+    pw, ph = [176, 88, 88], [144, 72, 72]
+    res = bench.frame_gather(d, coll_dev, parsed, 176 * 144 * 3 // 2, copy_frame, pw, ph, gathered, 2)
+    if rank == 0:
+        q.put((parity, res, [len(g) for g in gathered]))
+    d.barrier()
+    d.destroy_process_group()
+
+
+@pytest.mark.parametrize("bad_rank", [-1, 1])
+def test_bench_distributed_phases_gloo(bad_rank):
+    """bench.py's N > 1 code (the functions the nccl run calls, here over gloo on CPU tensors):
+    every rank's digests reach rank 0, parity is bit-exact -- or names the rank whose digests
+    differ -- and the rank-0 frame gather of two GOPs per rank verifies in display order."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bench_phase_worker, args=(r, world, port, q, bad_rank)) for r in range(world)]
+    for p in procs:
+        p.start()
+    parity, res, lens = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert lens == [18, 18]
+    if bad_rank < 0:
+        assert parity["status"] == "bit-exact" and parity["frames_checked"] == 36
+    else:
+        assert parity == {"status": "MISMATCH", "ranks_mismatching": [bad_rank]}
+    assert res["verified"] and res["frames"] == 2 * 2 * 6
+
+
+def test_gather_gops_sends_on_the_backend_device():
+    """Every frame handed to the grouped send is on the backend's device (gather_gops copies a
+    frame from another device first: a cuda frame under gloo, a host frame under nccl); here with
+    a stand-in distributed module that records what it is asked to send."""
+    import sys
+    sys.path[:0] = [REPO]
+    import torch
+    from tiny_mp2v_dec_amd import gather as G
+
+    sent = []
+
+    class FakeDist:
+        isend, irecv = "isend", "irecv"
+
+        @staticmethod
+        def get_rank():
+            return 1
+
+        @staticmethod
+        def get_world_size():
+            return 2
+
+        class P2POp:
+            def __init__(self, op, t, peer):
+                sent.append((op, t, peer))
+
+        @staticmethod
+        def batch_isend_irecv(ops):
+            return []
+
+    frames = {1: [torch.zeros(8, dtype=torch.uint8), torch.ones(8, dtype=torch.uint8)]}
+    G.gather_gops(FakeDist, frames, [3, 2], 8, device="cpu")
+    assert [(op, peer) for op, _, peer in sent] == [("isend", 0), ("isend", 0)]
+    assert all(t.device == torch.device("cpu") for _, t, _ in sent)
+
+
+@pytest.mark.parametrize("config,ranks", [("c2", 8), ("c4", 8)])
+def test_reference_digests_for_every_rank_of_the_scaling_run(config, ranks):
+    """The driver's 1/2/4/8-GPU bench runs give rank r the stream of seed 1729 + r: the compiled
+    reference's per-frame digests exist for every rank, so parity is checked on all of them."""
+    import sys
+    sys.path[:0] = [REPO]
+    import bench
+    for r in range(ranks):
+        exp = bench.expected_digests(config, bench.DEFAULT_GOPS[config], 1729 + r)
+        assert exp is not None and len(exp) == 12 * bench.DEFAULT_GOPS[config], (config, r)

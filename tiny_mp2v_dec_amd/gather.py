@@ -64,6 +64,13 @@ def gather_gops(dist, gop_frames, gop_sizes, frame_bytes, device="cpu", dst=0):
     rank = dist.get_rank() if dist is not None else 0
     world = dist.get_world_size() if dist is not None else 1
     owner = gop_owner(len(gop_sizes), world)
+    dev = torch.device(device)
+
+    def on_backend_device(f):
+        # a frame on another device than the backend moves (e.g. a cuda tensor under gloo, or a
+        # host tensor under nccl) is copied over first: batch_isend_irecv needs one device
+        return f if f.device == dev else f.to(dev)
+
     out = [] if rank == dst else None
     for r0 in range(0, len(gop_sizes), world):
         ops, recv = [], {}
@@ -71,12 +78,12 @@ def gather_gops(dist, gop_frames, gop_sizes, frame_bytes, device="cpu", dst=0):
             o = owner[g]
             if o == dst:
                 if rank == dst:
-                    recv[g] = list(gop_frames[g])
+                    recv[g] = [on_backend_device(f) for f in gop_frames[g]]
                 continue
             if rank == o:
                 if len(gop_frames[g]) != gop_sizes[g]:
                     raise ValueError(f"GOP {g}: {len(gop_frames[g])} frames, expected {gop_sizes[g]}")
-                ops += [dist.P2POp(dist.isend, f, dst) for f in gop_frames[g]]
+                ops += [dist.P2POp(dist.isend, on_backend_device(f), dst) for f in gop_frames[g]]
             elif rank == dst:
                 bufs = [torch.empty(frame_bytes, dtype=torch.uint8, device=device) for _ in range(gop_sizes[g])]
                 ops += [dist.P2POp(dist.irecv, b, o) for b in bufs]
