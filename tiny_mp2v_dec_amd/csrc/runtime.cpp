@@ -243,7 +243,8 @@ extern "C" int mp2vg_reserve_slots(mp2vg_ctx_t* c, int32_t nslots) {
 // Validate the batch so no kernel access can leave its buffers, and compute dependency levels.
 static int plan_batch(mp2vg_ctx_t* c, const mp2vg_picture_t* pics, int32_t npics, const mp2vg_mb_t* mbs,
                       uint64_t nmbs, const uint32_t* coefs, uint64_t ncoefs, std::vector<SliceDesc>& slices,
-                      std::vector<Launch>& launches, std::vector<std::vector<int32_t>>* foot = nullptr) {
+                      std::vector<Launch>& launches, std::vector<std::vector<int32_t>>* foot = nullptr,
+                      bool trusted = false) {
     const int mbw = c->cfg.width / 16, mbh = c->cfg.height / 16;
     const int nb = c->g.nblocks;
     // the I kernels address coefficient words with 32-bit byte offsets (a buffer resource)
@@ -258,7 +259,30 @@ static int plan_batch(mp2vg_ctx_t* c, const mp2vg_picture_t* pics, int32_t npics
     // failing picture in batch order reports its error
     std::vector<uint8_t> uses_of(2 * (size_t)npics, 0);
     std::vector<const char*> err(npics, nullptr);
+    // records of this library's own parser (the drop-in decoder) meet the contract by
+    // construction (tests/test_validate.py: parsed batches validate): only the picture-level checks
+    // and the reference usage the scheduler needs are computed for them
+    auto uses_only = [&](int p) -> const char* {
+        const mp2vg_picture_t& P = pics[p];
+        if (P.mb_width != mbw || P.mb_height != mbh) return "picture size differs from the context geometry";
+        if (P.dst_slot < 0 || P.dst_slot >= c->nslots || P.fwd_slot >= c->nslots || P.bwd_slot >= c->nslots)
+            return "frame slot out of range (mp2vg_reserve_slots)";
+        const uint64_t nm = (uint64_t)mbw * mbh;
+        if ((uint64_t)P.mb_first + nm > nmbs) return "picture MB range outside the batch";
+        bool uses[2] = {false, false};
+        for (uint64_t k = 0; k < nm; k++) {
+            const uint16_t f = mbs[P.mb_first + k].flags;
+            if (!(f & MP2VG_MB_INTRA)) {
+                uses[0] |= (f & MP2VG_MB_FWD) || !(f & MP2VG_MB_BWD);
+                uses[1] |= (f & MP2VG_MB_BWD) != 0;
+            }
+        }
+        uses_of[2 * (size_t)p] = uses[0];
+        uses_of[2 * (size_t)p + 1] = uses[1];
+        return nullptr;
+    };
     auto validate = [&](int p) -> const char* {
+        if (trusted) return uses_only(p);
         const mp2vg_picture_t& P = pics[p];
         if (P.mb_width != mbw || P.mb_height != mbh) return "picture size differs from the context geometry";
         if (P.dst_slot < 0 || P.dst_slot >= c->nslots || P.fwd_slot >= c->nslots || P.bwd_slot >= c->nslots)
@@ -448,7 +472,8 @@ static int plan_batch(mp2vg_ctx_t* c, const mp2vg_picture_t* pics, int32_t npics
 }
 
 static int batch_upload(mp2vg_ctx_t* c, const mp2vg_picture_t* pics, int32_t npics, const mp2vg_mb_t* mbs,
-                        uint64_t nmbs, const uint32_t* coefs, uint64_t ncoefs, bool pinned, bool async) {
+                        uint64_t nmbs, const uint32_t* coefs, uint64_t ncoefs, bool pinned, bool async,
+                        bool trusted = false) {
     if (!c || !pics || npics <= 0 || !mbs || (!coefs && ncoefs)) return MP2VG_E_INVALID;
     HIPCHK(hipSetDevice(c->cfg.device));
     c->batch_ready = false;
@@ -456,7 +481,7 @@ static int batch_upload(mp2vg_ctx_t* c, const mp2vg_picture_t* pics, int32_t npi
     std::vector<Launch> lb;
     std::vector<std::vector<int32_t>> foot;
     double tp = now_ms();
-    int rc = plan_batch(c, pics, npics, mbs, nmbs, coefs, ncoefs, slices, lb, &foot);
+    int rc = plan_batch(c, pics, npics, mbs, nmbs, coefs, ncoefs, slices, lb, &foot, trusted);
     if (rc != MP2VG_OK) return rc;
     tp = trace_phase("upload: plan", tp);
     // the other bank from the last upload; the decode queued on it is still allowed to run
@@ -521,10 +546,11 @@ extern "C" int mp2vg_batch_upload(mp2vg_ctx_t* c, const mp2vg_picture_t* pics, i
 namespace mp2vg {
 // Drop-in decoder (decoder.cpp): records in pinned host memory go to the device without staging
 // and without waiting for the copies.  Its pinned buffer set i feeds bank i (banks alternate per
-// upload): before rewriting set ctx_next_bank(), it calls ctx_wait_upload(ctx, that bank).
+// upload): before rewriting set ctx_next_bank(), it calls ctx_wait_upload(ctx, that bank).  The
+// records come from this library's parser, so the per-macroblock validation is skipped (trusted).
 int batch_upload_pinned(mp2vg_ctx_t* c, const mp2vg_picture_t* pics, int32_t npics, const mp2vg_mb_t* mbs,
                         uint64_t nmbs, const uint32_t* coefs, uint64_t ncoefs) {
-    return batch_upload(c, pics, npics, mbs, nmbs, coefs, ncoefs, true, true);
+    return batch_upload(c, pics, npics, mbs, nmbs, coefs, ncoefs, true, true, true);
 }
 int ctx_next_bank(const mp2vg_ctx_t* c) { return (c->cur + 1) & 1; }
 int ctx_wait_upload(mp2vg_ctx_t* c, int bank) {
