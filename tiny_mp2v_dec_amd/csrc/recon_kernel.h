@@ -1,20 +1,21 @@
 // recon_kernel.h — device side of the macroblock reconstruct path (gfx950 / CDNA4).
 //
-// One workgroup (4 waves) per slice = MB row; each wave reconstructs whole macroblocks
-// independently (MBs w, w+4, w+8, ... of the row) with wave-private LDS, so no workgroup barrier
-// sits in the MB loop.  Per macroblock:
+// One workgroup (4 waves) per slice = MB row (XCD-aware slice order); each wave reconstructs
+// groups of 4 consecutive macroblocks (groups w, w+4, w+8, ... of the row) with wave-private LDS,
+// so no workgroup barrier sits in the loop, which is software-pipelined one group ahead.  Per
+// group (recon.hip has the details):
 //   1. dequant + mismatch control         reference mb_decoder.cpp:74-155 (parse_block)
-//      lanes = coefficient words (coalesced 4-B loads), LDS scatter into a per-block raster,
-//      mismatch parity by LDS xor atomics.
+//      lane = coefficient word (coalesced 4-B loads, prefetched one group ahead), scattered into
+//      compacted coded-block slots in LDS through a per-group dequant table.
 //   2. IDCT, SSE2-exact                    reference idct_sse2.hpp:23-120
-//      lane = (block, line): pass 1 over the horizontal frequency (one 16-B LDS row read),
-//      LDS transpose, pass 2, >>6 -> residual image in LDS with the dct_type placement of
-//      mb_decoder.cpp:166-196.
+//      lane = two lines of one block on packed i16 pairs; the block parity (mismatch control)
+//      is reduced over the block's 4 lanes with ds_swizzle; pass 1, transpose in LDS, pass 2,
+//      >>6 -> residual image with the dct_type placement of mb_decoder.cpp:166-196.
 //   3. MC + add/clip + store               reference mb_decoder.cpp:198-339, mc_sse2.hpp,
 //      idct_sse2.hpp:106-119 (packus / adds+packus)
-//      lane = 4 horizontally adjacent pixels: 4-byte SWAR half-pel averaging with the
-//      reference's cascaded rounding, bidirectional average, residual add + clamp, one
-//      4-byte store.
+//      lane = one pixel row (16-px luma, 8/16-px chroma): reference rows by raw buffer loads
+//      issued one group ahead, cascaded half-pel averages with v_lerp_u8 (== _mm_avg_epu8),
+//      bidirectional average, residual add + clamp on packed i16, one 16-B / 8-B row store.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
