@@ -85,10 +85,35 @@ struct NoInitAlloc : std::allocator<T> {
     }
 };
 
-using CoefVec = std::vector<uint32_t, NoInitAlloc<uint32_t>>;
+// A slice's coefficient words: grown without zeroing and written through a raw pointer into a
+// per-MB worst-case reservation (a std::vector resize per macroblock was 4 % of the parse)
+struct CoefVec {
+    uint32_t* d = nullptr;
+    size_t n = 0, cap = 0;
+    CoefVec() = default;
+    CoefVec(const CoefVec&) = delete;
+    CoefVec& operator=(const CoefVec&) = delete;
+    CoefVec(CoefVec&& o) noexcept : d(o.d), n(o.n), cap(o.cap) { o.d = nullptr, o.n = o.cap = 0; }
+    ~CoefVec() { free(d); }
+    void swap(CoefVec& o) noexcept { std::swap(d, o.d), std::swap(n, o.n), std::swap(cap, o.cap); }
+    uint32_t* data() { return d; }
+    const uint32_t* data() const { return d; }
+    size_t size() const { return n; }
+    bool empty() const { return n == 0; }
+    // room for at least `need` words (contents kept)
+    bool reserve(size_t need) {
+        if (need <= cap) return true;
+        size_t c = std::max<size_t>(need, 2 * cap);
+        uint32_t* nd = (uint32_t*)realloc(d, c * sizeof(uint32_t));
+        if (!nd) return false;
+        d = nd;
+        cap = c;
+        return true;
+    }
+};
 
 struct SliceOut {
-    CoefVec coefs;  // grown without zeroing; written through a raw pointer
+    CoefVec coefs;
     int mb_row = -1;
     int status = MP2VG_OK;
     std::string err;
@@ -119,8 +144,9 @@ void parse_slice(const Ctx& C, const PicWork& P, const SliceJob& job, mp2vg_mb_t
     const int pct = h.pct;
     const int cf = C.g.cf;
     const int nblocks = C.g.nblocks;
-    BitReader br(C.buf + job.byte_off, C.buf + job.byte_end);
-    out.coefs.reserve(4096);
+    // the reader continues past the slice into the bytes after it, as the reference's does
+    BitReader br(C.buf + job.byte_off, C.buf + job.byte_end, C.buf + C.len);
+    if (!out.coefs.reserve(4096)) FAIL(MP2VG_E_NOMEM, "out of host memory");
 
     // slice header (mp2v_hdr.h:345-363)
     br.skip(24);
@@ -155,7 +181,7 @@ void parse_slice(const Ctx& C, const PicWork& P, const SliceJob& job, mp2vg_mb_t
     const int pstruct_frame = 1;  // only frame pictures are accepted
     (void)pstruct_frame;
 
-    auto emit_skipped = [&](int xx) -> bool {
+    auto emit_skipped = [&](int xx) __attribute__((always_inline)) -> bool {
         mp2vg_mb_t& m = row[xx];
         memset(&m, 0, sizeof(m));
         m.x = (uint16_t)xx;
@@ -234,7 +260,9 @@ void parse_slice(const Ctx& C, const PicWork& P, const SliceJob& job, mp2vg_mb_t
         // motion_vectors (mb_decoder.cpp:479-519, 565-574)
         int16_t MVs[2][2][2] = {};
         int fsel[2][2] = {};
-        auto parse_mv = [&](int r, int s) -> bool {
+        // (always inline: an out-of-line lambda takes br's address and keeps the slice's bit
+        // reader in memory, a store-forwarding round trip on every read)
+        auto parse_mv = [&](int r, int s) __attribute__((always_inline)) -> bool {
             for (int t = 0; t < 2; t++) {
                 int ci = T.motion.decode(br);
                 if (ci < 0) return false;
@@ -247,7 +275,7 @@ void parse_slice(const Ctx& C, const PicWork& P, const SliceJob& job, mp2vg_mb_t
             }
             return true;
         };
-        auto parse_mvs = [&](int s) -> bool {
+        auto parse_mvs = [&](int s) __attribute__((always_inline)) -> bool {
             if (mv_count == 1) {
                 if (field_mv) fsel[0][s] = (int)br.read(1);
                 return parse_mv(0, s);
@@ -346,9 +374,14 @@ void parse_slice(const Ctx& C, const PicWork& P, const SliceJob& job, mp2vg_mb_t
         const CoefLut& cf_lut = T.coefs[tab];
         // room for the MB's worst case (64 words per coded block), written through a raw pointer
         const size_t n0 = out.coefs.size();
-        out.coefs.resize(n0 + 64 * (size_t)__builtin_popcount(cbp));
+        if (!out.coefs.reserve(n0 + 64 * (size_t)__builtin_popcount(cbp))) FAIL(MP2VG_E_NOMEM, "out of host memory");
         uint32_t* w = out.coefs.data() + n0;
         const uint32_t mbx_tag = MP2VG_COEF_MBX(x);
+        // the block loop decodes from a local copy of the reader (its address never escapes, so
+        // the cache, bit count and pointer stay in registers) and hands it back at the end
+        BitReader r = br;
+        const uint32_t* const lut1 = cf_lut.l1.data();
+        const uint32_t* const lut2 = cf_lut.l2.data();
         for (int b = 0; b < nblocks; b++) {
             if (!(cbp & (1u << b))) continue;
             int i = 0;
@@ -356,12 +389,12 @@ void parse_slice(const Ctx& C, const PicWork& P, const SliceJob& job, mp2vg_mb_t
             if (intra) {
                 // parse_dct_dc_coeff (mb_decoder.cpp:46-72)
                 int pidx = b < 4 ? 0 : ((b & 1) ? 2 : 1);
-                int si = (b < 4 ? T.dc_luma : T.dc_chroma).decode(br);
+                int si = (b < 4 ? T.dc_luma : T.dc_chroma).decode(r);
                 if (si < 0) FAIL(MP2VG_E_BITSTREAM, "bad dct_dc_size");
                 int size = (b < 4 ? kDcSizeLuma : kDcSizeChroma)[si].a;
                 int diff = 0;
                 if (size) {
-                    int d = (int)br.read(size);
+                    int d = (int)r.read(size);
                     int half = 1 << (size - 1);
                     diff = d >= half ? d : (d + 1) - 2 * half;
                 }
@@ -371,18 +404,19 @@ void parse_slice(const Ctx& C, const PicWork& P, const SliceJob& job, mp2vg_mb_t
                 i = 1;
             } else {
                 // non-intra first coefficient '1s' (mb_decoder.cpp:79-88)
-                uint32_t c = br.peek(2);
+                uint32_t c = r.peek(2);
                 if (c & 2) {
                     int lvl = (c & 1) ? -1 : 1;
                     *w++ = MP2VG_COEF_PACK(lvl, 0, b, MP2VG_COEF_FIRST1S | MP2VG_COEF_MBX(x));
-                    br.skip(2);
+                    r.skip(2);
                     i = 1;
                 }
             }
             // parse_block's VLC loop (mb_decoder.cpp:89-149): one refill per code
             for (;;) {
                 int run, level;
-                const int kind = cf_lut.decode(br, run, level);
+                r.refill();
+                const int kind = CoefLut::decode_tab(lut1, lut2, r, run, level);
                 if (kind != CoefLut::NORMAL) {  // escapes come back as NORMAL (:100-104)
                     if (kind < 0) FAIL(MP2VG_E_BITSTREAM, "bad DCT coefficient code");
                     break;  // EOB
@@ -393,7 +427,8 @@ void parse_slice(const Ctx& C, const PicWork& P, const SliceJob& job, mp2vg_mb_t
                 i++;
             }
         }
-        out.coefs.resize((size_t)(w - out.coefs.data()));
+        br = r;
+        out.coefs.n = (size_t)(w - out.coefs.data());
         size_t nc = out.coefs.size() - m.coef_off;
         m.ncoef = (uint16_t)nc;
         if (br.overrun()) FAIL(MP2VG_E_BITSTREAM, "slice overruns the buffer");

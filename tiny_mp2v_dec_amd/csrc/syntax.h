@@ -15,34 +15,44 @@
 namespace mp2vg {
 
 // ---------------------------------------------------------------------------------------------
-// MSB-first bit reader over a byte buffer (zeros past the end).  Plays the role of the
-// reference's bitstream_reader_c (bitstream.h:22-64); peek(n) for n <= 32.
+// MSB-first bit reader over a byte buffer.  Plays the role of the reference's
+// bitstream_reader_c (bitstream.h:22-64), which also reads on past a slice's end into the bytes
+// that follow it; peek(n) for n <= 32.  The bits are those of [b, hard_end), then zeros; `end`
+// (<= hard_end) is the unit being parsed (a slice), which overrun() checks against.
 struct BitReader {
     const uint8_t* base = nullptr;
     const uint8_t* p = nullptr;
     const uint8_t* end = nullptr;
+    const uint8_t* hend = nullptr;  // bytes at or past hend read as 0
+    const uint8_t* lim = nullptr;   // last p with an 8-byte load inside [base, hend)
     uint64_t cache = 0;
-    int bits = 0;  // valid bits in cache (MSB aligned)
+    int bits = 0;  // valid bits in cache (MSB aligned); the bits below them are the stream's next
 
     BitReader() = default;
-    BitReader(const uint8_t* b, const uint8_t* e) : base(b), p(b), end(e) {}
+    BitReader(const uint8_t* b, const uint8_t* e) : BitReader(b, e, e) {}
+    BitReader(const uint8_t* b, const uint8_t* e, const uint8_t* hard_end)
+        : base(b), p(b), end(e), hend(hard_end), lim(hard_end - b >= 8 ? hard_end - 8 : nullptr) {}
 
-    // Keeps >= 32 valid bits after a refill.  Fast path: one unaligned 8-byte big-endian load
-    // adds as many whole bytes as fit; near the end of the buffer, bytes past `end` read as 0.
+    // Leaves 56-63 valid bits.  Branch-free fast path (no test on `bits`, whose pattern is
+    // unpredictable): one unaligned 8-byte big-endian load ORed in below the valid bits, p
+    // advanced by the whole bytes that fit.  The bits it leaves below the valid ones are the
+    // stream's next bits, so ORing them again later changes nothing.
     inline void refill() {
-        if (bits > 32) return;
-        if (p + 8 <= end) {
+        if (__builtin_expect(p <= lim, 1)) {
             uint64_t v;
             memcpy(&v, p, 8);
-            v = __builtin_bswap64(v);
-            const int k = (63 - bits) >> 3;  // 3..7 whole bytes
-            cache |= (v >> (8 * (8 - k))) << (64 - bits - 8 * k);
-            p += k;
-            bits += 8 * k;
+            cache |= __builtin_bswap64(v) >> bits;
+            p += (63 - bits) >> 3;
+            bits |= 56;
             return;
         }
+        refill_tail();
+    }
+    // (inline: an out-of-line call would take the reader's address and pin a hot loop's local
+    // reader to the stack)
+    inline void refill_tail() {
         while (bits <= 56) {
-            uint64_t byte = (p < end) ? *p : 0;
+            uint64_t byte = (p < hend) ? *p : 0;
             cache |= byte << (56 - bits);
             p++;
             bits += 8;
@@ -169,20 +179,29 @@ struct CoefLut {
     }
     // after a refill; consumes at most 24 bits
     inline int decode_nr(BitReader& br, int& run, int& level) const {
-        uint32_t e = l1[br.peek_nr(L1)];
+        return decode_tab(l1.data(), l2.data(), br, run, level);
+    }
+    // the same on table pointers held by the caller (a hot loop keeps them, and its local
+    // BitReader, in registers)
+    static inline int decode_tab(const uint32_t* t1, const uint32_t* t2, BitReader& br, int& run, int& level) {
+        uint32_t e = t1[br.peek_nr(L1)];
         if (__builtin_expect(((e >> 23) & 3) == SUB, 0)) {
             br.skip_nr(L1);
-            e = l2[(((e >> 5) & 0x3ffff) << L2) + br.peek_nr(L2)];
+            e = t2[(((e >> 5) & 0x3ffff) << L2) + br.peek_nr(L2)];
         }
         const int len = (int)(e & 31);
         if (__builtin_expect(!len, 0)) return -1;
         const int kind = (int)((e >> 23) & 3);
-        const bool esc = kind == ESC;                             // the escape code is 6 bits
-        const uint32_t x = (uint32_t)((br.cache << 6) >> 46);     // the 18 bits after it
-        run = esc ? (int)(x >> 12) : (int)((e >> 5) & 63);
-        level = esc ? ((int32_t)(x << 20) >> 20) : (int)((int32_t)(e << 9) >> 20);  // signed 12 bits
-        br.skip_nr(len + (esc ? 18 : 0));
-        return esc ? (int)NORMAL : kind;
+        // escape (6-bit code, then 6-bit run and signed 12-bit level) without a branch: masks
+        // select between the entry's (run, level) and the 18 bits after the escape code
+        const uint32_t esc = 0u - (uint32_t)(kind == ESC);
+        const uint32_t x = (uint32_t)((br.cache << 6) >> 46);
+        const uint32_t rl_norm = (e >> 5) & 0x3ffffu;  // run (6 b) | level (12 b) << 6
+        const uint32_t rl = (rl_norm & ~esc) | (((x >> 12) | ((x & 0xfffu) << 6)) & esc);
+        run = (int)(rl & 63);
+        level = (int32_t)(rl << 14) >> 20;  // signed 12 bits
+        br.skip_nr(len + (int)(esc & 18u));
+        return kind & ~(int)(esc & 2u);  // ESC -> NORMAL
     }
 };
 
