@@ -700,6 +700,8 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, LT&
     using RL = ResLayout<CF>;
     constexpr int NB = F::NB;
     constexpr int NWC = F::CW / 4;
+    // 4:2:0 intra groups (24 blocks) run both IDCT passes in shared rounds (D' below)
+    constexpr bool UNI = LT::COMPACT && CF == 1;
     const uint32_t mb_end = c.mb_end, mb_last = c.mb_end - 1;
     uint32_t g = c.mb_begin + wave * G;
     if (g >= mb_end) return;
@@ -816,81 +818,147 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, LT&
         wave_sync();
 
         stamp<ABL>(st, 2);
-        // ---- D. IDCT pass 1 (idct_sse2.hpp:102-103): lane (slot, v, v+1) transforms coefficient
-        //         rows v, v+1 over u.  Mismatch control (mb_decoder.cpp:150-152; intra DC
-        //         excluded, :76) is folded in: the block parity is reduced over the slot's 4
-        //         lanes with ds_swizzle and applied to QFS[63] (row 7, u 7) before the
-        //         transform.  Output transposed in place ([x][v]): the block is read by one
-        //         ds_read instruction before any lane writes it.
-        for (int t = lane; t < ((ABL & 1) ? 0 : S.nslots * 4); t += 64) {
-            const int slot = t >> 2, v = (t & 3) * 2;
-            short* const bw = (short*)L.blk[wave];
-            uint4 ra = *(const uint4*)&bw[LT::bofs(slot, v * 8)];
-            uint4 rb = *(const uint4*)&bw[LT::bofs(slot, v * 8 + 8)];
-            const int k = L.map[wave][slot] >> 4;
-            const bool intra = pick8(S.fl8, k) & MP2VG_MB_INTRA;
-            uint32_t par = (ra.x ^ ra.y ^ ra.z ^ ra.w ^ rb.x ^ rb.y ^ rb.z ^ rb.w) & 0x00010001u;
-            if (v == 0 && intra) par ^= ra.x & 1u;  // DC excluded
-            par = (par ^ (par >> 16)) & 1u;
-            par ^= (uint32_t)__builtin_amdgcn_ds_swizzle((int)par, 0x041F);  // xor lane 1
-            par ^= (uint32_t)__builtin_amdgcn_ds_swizzle((int)par, 0x081F);  // xor lane 2
-            if (v == 6) rb.w ^= (par ^ 1u) << 16;  // sum even -> toggle the LSB of QFS[63]
-            // pair-interleaved block: dword u = (row v, row v + 1) of column u, no unpacking
-            short2_t s[8] = {__builtin_bit_cast(short2_t, ra.x), __builtin_bit_cast(short2_t, ra.y),
-                             __builtin_bit_cast(short2_t, ra.z), __builtin_bit_cast(short2_t, ra.w),
-                             __builtin_bit_cast(short2_t, rb.x), __builtin_bit_cast(short2_t, rb.y),
-                             __builtin_bit_cast(short2_t, rb.z), __builtin_bit_cast(short2_t, rb.w)};
-            idct_1d(s);
-#pragma unroll
-            for (int x = 0; x < 8; x++) *(short2_t*)&bw[LT::bofs(slot, x * 8 + v)] = s[x];
-        }
-        wave_sync();
-        // chroma taps of g+1 issued mid-iteration: spreads the wave's TA demand
-        __builtin_amdgcn_sched_barrier(0);
-        if (MCM) {
-            issue_pass<CF, MCM, 1, NWC, ABL>(R, gliveN, lane, geo, c.ref_fwd, c.ref_bwd, t1f, t1b);
-            if (CF != 1) issue_pass<CF, MCM, 2, NWC, ABL>(R, gliveN, lane, geo, c.ref_fwd, c.ref_bwd, t2f, t2b);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        stamp<ABL>(st, 3);
-        // pass 2 (:104-108): lane (slot, x, x+2) transforms columns x, x+2 over v; >>6 -> residual
-        // image in the MB's dct_type placement (:166-196); the block area is zeroed for the next
-        // group
-        for (int t = lane; t < ((ABL & 1) ? 0 : S.nslots * 4); t += 64) {
-            const int slot = t >> 2, xq = t & 3;
-            const int x = (xq & 1) | ((xq & 2) << 1);  // 0, 1, 4, 5
-            short* const bw = (short*)L.blk[wave];
-            const uint4 ra = *(const uint4*)&bw[LT::bofs(slot, x * 8)];
-            const uint4 rb = *(const uint4*)&bw[LT::bofs(slot, x * 8 + 16)];
-            *(uint4*)&bw[LT::bofs(slot, x * 8)] = make_uint4(0, 0, 0, 0);
-            *(uint4*)&bw[LT::bofs(slot, x * 8 + 16)] = make_uint4(0, 0, 0, 0);
-            short2_t s[8];
-            interleave(ra, rb, s);
-            idct_1d(s);
-            const int kb = L.map[wave][slot];
-            const int k = kb >> 4, bb = kb & 15;
-            const bool dctf = pick8(S.fl8, k) & MP2VG_MB_DCT_FIELD;
-            int plane, x0, y0, ys;
-            block_origin<CF>(bb, dctf, plane, x0, y0, ys);
-            const int rw = RL::width(plane);
-            const int xp = RL::pos(x0 + x);  // (x, x+2) -> (xp, xp+1)
-            if constexpr (LT::COMPACT) {
-                // intra put (idct_sse2.hpp:106-108): packus(res) -- the clamped bytes of (x, x+2)
-                uint8_t* res8 = (uint8_t*)L.res[wave] + k * RL::SIZE + RL::base(plane);
-                const short2_t z = {0, 0}, m = {255, 255};
-#pragma unroll
-                for (int y = 0; y < 8; y++) {
-                    const short2_t t = __builtin_elementwise_min(__builtin_elementwise_max(s[y] >> (short)6, z), m);
-                    *(uint16_t*)&res8[(y0 + y * ys) * rw + xp] =
-                        (uint16_t)__builtin_amdgcn_perm(0u, __builtin_bit_cast(uint32_t, t), 0x0c0c0200u);
-                }
-            } else {
-                short* res = &L.res[wave][k * RL::SIZE + RL::base(plane)];
-#pragma unroll
-                for (int y = 0; y < 8; y++) *(short2_t*)&res[(y0 + y * ys) * rw + xp] = s[y] >> (short)6;
+        if constexpr (!UNI) {
+            // ---- D. IDCT pass 1 (idct_sse2.hpp:102-103): lane (slot, v, v+1) transforms coefficient
+            //         rows v, v+1 over u.  Mismatch control (mb_decoder.cpp:150-152; intra DC
+            //         excluded, :76) is folded in: the block parity is reduced over the slot's 4
+            //         lanes with ds_swizzle and applied to QFS[63] (row 7, u 7) before the
+            //         transform.  Output transposed in place ([x][v]): the block is read by one
+            //         ds_read instruction before any lane writes it.
+            for (int t = lane; t < ((ABL & 1) ? 0 : S.nslots * 4); t += 64) {
+                const int slot = t >> 2, v = (t & 3) * 2;
+                short* const bw = (short*)L.blk[wave];
+                uint4 ra = *(const uint4*)&bw[LT::bofs(slot, v * 8)];
+                uint4 rb = *(const uint4*)&bw[LT::bofs(slot, v * 8 + 8)];
+                const int k = L.map[wave][slot] >> 4;
+                const bool intra = pick8(S.fl8, k) & MP2VG_MB_INTRA;
+                uint32_t par = (ra.x ^ ra.y ^ ra.z ^ ra.w ^ rb.x ^ rb.y ^ rb.z ^ rb.w) & 0x00010001u;
+                if (v == 0 && intra) par ^= ra.x & 1u;  // DC excluded
+                par = (par ^ (par >> 16)) & 1u;
+                par ^= (uint32_t)__builtin_amdgcn_ds_swizzle((int)par, 0x041F);  // xor lane 1
+                par ^= (uint32_t)__builtin_amdgcn_ds_swizzle((int)par, 0x081F);  // xor lane 2
+                if (v == 6) rb.w ^= (par ^ 1u) << 16;  // sum even -> toggle the LSB of QFS[63]
+                // pair-interleaved block: dword u = (row v, row v + 1) of column u, no unpacking
+                short2_t s[8] = {__builtin_bit_cast(short2_t, ra.x), __builtin_bit_cast(short2_t, ra.y),
+                                 __builtin_bit_cast(short2_t, ra.z), __builtin_bit_cast(short2_t, ra.w),
+                                 __builtin_bit_cast(short2_t, rb.x), __builtin_bit_cast(short2_t, rb.y),
+                                 __builtin_bit_cast(short2_t, rb.z), __builtin_bit_cast(short2_t, rb.w)};
+                idct_1d(s);
+    #pragma unroll
+                for (int x = 0; x < 8; x++) *(short2_t*)&bw[LT::bofs(slot, x * 8 + v)] = s[x];
             }
+            wave_sync();
+            // chroma taps of g+1 issued mid-iteration: spreads the wave's TA demand
+            __builtin_amdgcn_sched_barrier(0);
+            if (MCM) {
+                issue_pass<CF, MCM, 1, NWC, ABL>(R, gliveN, lane, geo, c.ref_fwd, c.ref_bwd, t1f, t1b);
+                if (CF != 1) issue_pass<CF, MCM, 2, NWC, ABL>(R, gliveN, lane, geo, c.ref_fwd, c.ref_bwd, t2f, t2b);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            stamp<ABL>(st, 3);
+            // pass 2 (:104-108): lane (slot, x, x+2) transforms columns x, x+2 over v; >>6 -> residual
+            // image in the MB's dct_type placement (:166-196); the block area is zeroed for the next
+            // group
+            for (int t = lane; t < ((ABL & 1) ? 0 : S.nslots * 4); t += 64) {
+                const int slot = t >> 2, xq = t & 3;
+                const int x = (xq & 1) | ((xq & 2) << 1);  // 0, 1, 4, 5
+                short* const bw = (short*)L.blk[wave];
+                const uint4 ra = *(const uint4*)&bw[LT::bofs(slot, x * 8)];
+                const uint4 rb = *(const uint4*)&bw[LT::bofs(slot, x * 8 + 16)];
+                *(uint4*)&bw[LT::bofs(slot, x * 8)] = make_uint4(0, 0, 0, 0);
+                *(uint4*)&bw[LT::bofs(slot, x * 8 + 16)] = make_uint4(0, 0, 0, 0);
+                short2_t s[8];
+                interleave(ra, rb, s);
+                idct_1d(s);
+                const int kb = L.map[wave][slot];
+                const int k = kb >> 4, bb = kb & 15;
+                const bool dctf = pick8(S.fl8, k) & MP2VG_MB_DCT_FIELD;
+                int plane, x0, y0, ys;
+                block_origin<CF>(bb, dctf, plane, x0, y0, ys);
+                const int rw = RL::width(plane);
+                const int xp = RL::pos(x0 + x);  // (x, x+2) -> (xp, xp+1)
+                if constexpr (LT::COMPACT) {
+                    // intra put (idct_sse2.hpp:106-108): packus(res) -- the clamped bytes of (x, x+2)
+                    uint8_t* res8 = (uint8_t*)L.res[wave] + k * RL::SIZE + RL::base(plane);
+                    const short2_t z = {0, 0}, m = {255, 255};
+    #pragma unroll
+                    for (int y = 0; y < 8; y++) {
+                        const short2_t t = __builtin_elementwise_min(__builtin_elementwise_max(s[y] >> (short)6, z), m);
+                        *(uint16_t*)&res8[(y0 + y * ys) * rw + xp] =
+                            (uint16_t)__builtin_amdgcn_perm(0u, __builtin_bit_cast(uint32_t, t), 0x0c0c0200u);
+                    }
+                } else {
+                    short* res = &L.res[wave][k * RL::SIZE + RL::base(plane)];
+    #pragma unroll
+                    for (int y = 0; y < 8; y++) *(short2_t*)&res[(y0 + y * ys) * rw + xp] = s[y] >> (short)6;
+                }
+            }
+            wave_sync();
+        } else {
+            // ---- D'. 4:2:0 intra: both IDCT passes in shared rounds.  A group's 24 blocks are 96
+            //          pass-1 items and 96 pass-2 items; item slots 0..95 are pass 1, 96..191 pass
+            //          2, three rounds of 64 instead of two half-empty rounds per pass.  A pass-2
+            //          item always lands in a later round than its block's pass-1 items (it sits
+            //          >= 64 slots after them), so one wave_sync per round orders them; within a
+            //          round the two passes touch different blocks.  The per-item work is the
+            //          pass-1 / pass-2 code below, unchanged.
+            const int n4 = S.nslots * 4;
+            const int p2b = n4 > 64 ? n4 : 64;
+            short* const bw = (short*)L.blk[wave];
+            for (int base = 0; base < ((ABL & 1) ? 0 : p2b + n4); base += 64) {
+                const int t = base + lane;
+                const bool p1 = t < n4;
+                const int u = p1 ? t : t - p2b;
+                if (p1 || (t >= p2b && u < n4)) {
+                    const int slot = u >> 2, q = u & 3;
+                    const int v = q * 2;                           // pass 1: rows v, v+1
+                    const int x = (q & 1) | ((q & 2) << 1);       // pass 2: columns x, x+2 (0, 1, 4, 5)
+                    uint4 ra = *(const uint4*)&bw[LT::bofs(slot, p1 ? v * 8 : x * 8)];
+                    uint4 rb = *(const uint4*)&bw[LT::bofs(slot, p1 ? v * 8 + 8 : x * 8 + 16)];
+                    short2_t sv[8];
+                    if (p1) {
+                        // mismatch control (intra: DC excluded), as in pass 1 above
+                        uint32_t par = (ra.x ^ ra.y ^ ra.z ^ ra.w ^ rb.x ^ rb.y ^ rb.z ^ rb.w) & 0x00010001u;
+                        if (v == 0) par ^= ra.x & 1u;
+                        par = (par ^ (par >> 16)) & 1u;
+                        par ^= (uint32_t)__builtin_amdgcn_ds_swizzle((int)par, 0x041F);
+                        par ^= (uint32_t)__builtin_amdgcn_ds_swizzle((int)par, 0x081F);
+                        if (v == 6) rb.w ^= (par ^ 1u) << 16;
+                        sv[0] = __builtin_bit_cast(short2_t, ra.x), sv[1] = __builtin_bit_cast(short2_t, ra.y);
+                        sv[2] = __builtin_bit_cast(short2_t, ra.z), sv[3] = __builtin_bit_cast(short2_t, ra.w);
+                        sv[4] = __builtin_bit_cast(short2_t, rb.x), sv[5] = __builtin_bit_cast(short2_t, rb.y);
+                        sv[6] = __builtin_bit_cast(short2_t, rb.z), sv[7] = __builtin_bit_cast(short2_t, rb.w);
+                    } else {
+                        *(uint4*)&bw[LT::bofs(slot, x * 8)] = make_uint4(0, 0, 0, 0);
+                        *(uint4*)&bw[LT::bofs(slot, x * 8 + 16)] = make_uint4(0, 0, 0, 0);
+                        interleave(ra, rb, sv);
+                    }
+                    idct_1d(sv);
+                    if (p1) {
+#pragma unroll
+                        for (int xx = 0; xx < 8; xx++) *(short2_t*)&bw[LT::bofs(slot, xx * 8 + v)] = sv[xx];
+                    } else {
+                        const int kb = L.map[wave][slot];
+                        const int k = kb >> 4, bb = kb & 15;
+                        const bool dctf = pick8(S.fl8, k) & MP2VG_MB_DCT_FIELD;
+                        int plane, x0, y0, ys;
+                        block_origin<CF>(bb, dctf, plane, x0, y0, ys);
+                        const int rw = RL::width(plane);
+                        const int xp = RL::pos(x0 + x);
+                        uint8_t* res8 = (uint8_t*)L.res[wave] + k * RL::SIZE + RL::base(plane);
+                        const short2_t z = {0, 0}, m = {255, 255};
+#pragma unroll
+                        for (int y = 0; y < 8; y++) {
+                            const short2_t tt = __builtin_elementwise_min(__builtin_elementwise_max(sv[y] >> (short)6, z), m);
+                            *(uint16_t*)&res8[(y0 + y * ys) * rw + xp] =
+                                (uint16_t)__builtin_amdgcn_perm(0u, __builtin_bit_cast(uint32_t, tt), 0x0c0c0200u);
+                        }
+                    }
+                }
+                wave_sync();
+            }
+            stamp<ABL>(st, 3);
         }
-        wave_sync();
 
         stamp<ABL>(st, 4);
         // ---- E. prediction + residual, one row store per lane ----
