@@ -111,6 +111,14 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// _mm_packus_epi16 on one packed pair: gfx950's v_sat_pk_u8_i16 (VOP1, full rate) clamps both i16
+// halves to [0, 255] and packs them into bytes 0-1 (no clang builtin: inline asm)
+__device__ __forceinline__ uint32_t sat_pk_u8(short2_t v) {
+    uint32_t r;
+    asm("v_sat_pk_u8_i16 %0, %1" : "=v"(r) : "v"(__builtin_bit_cast(uint32_t, v)));
+    return r;
+}
+
 // per-byte (a + b + 1) >> 1 on 4 packed u8 == _mm_avg_epu8: one v_lerp_u8 (rounding bit per byte)
 __device__ __forceinline__ uint32_t avg4(uint32_t a, uint32_t b) { return __builtin_amdgcn_lerp(a, b, 0x01010101u); }
 
@@ -503,13 +511,10 @@ __device__ __forceinline__ void store_pass(uint32_t r0, uint32_t r1, bool live, 
             // pairs (x0, x0+2) and (x0+1, x0+3) as packed i16
             const uint32_t lo = __builtin_amdgcn_perm(0u, out[d], 0x0c020c00u);
             const uint32_t hi = __builtin_amdgcn_perm(0u, out[d], 0x0c030c01u);
-            short2_t a = __builtin_bit_cast(short2_t, lo) + __builtin_bit_cast(short2_t, rv[2 * d]);
-            short2_t c = __builtin_bit_cast(short2_t, hi) + __builtin_bit_cast(short2_t, rv[2 * d + 1]);
-            const short2_t z = {0, 0}, m = {255, 255};
-            a = __builtin_elementwise_min(__builtin_elementwise_max(a, z), m);
-            c = __builtin_elementwise_min(__builtin_elementwise_max(c, z), m);
-            // bytes: x0 = a.lo, x0+1 = c.lo, x0+2 = a.hi, x0+3 = c.hi
-            out[d] = __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, c), __builtin_bit_cast(uint32_t, a), 0x06020400u);
+            const short2_t a = __builtin_bit_cast(short2_t, lo) + __builtin_bit_cast(short2_t, rv[2 * d]);
+            const short2_t c = __builtin_bit_cast(short2_t, hi) + __builtin_bit_cast(short2_t, rv[2 * d + 1]);
+            // packus: bytes x0 = a.lo, x0+1 = c.lo, x0+2 = a.hi, x0+3 = c.hi
+            out[d] = __builtin_amdgcn_perm(sat_pk_u8(c), sat_pk_u8(a), 0x05010400u);
         }
     }
     const int pw = plane == 0 ? 16 : F::CW;
@@ -844,7 +849,7 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, LT&
                                  __builtin_bit_cast(short2_t, rb.x), __builtin_bit_cast(short2_t, rb.y),
                                  __builtin_bit_cast(short2_t, rb.z), __builtin_bit_cast(short2_t, rb.w)};
                 idct_1d(s);
-    #pragma unroll
+#pragma unroll
                 for (int x = 0; x < 8; x++) *(short2_t*)&bw[LT::bofs(slot, x * 8 + v)] = s[x];
             }
             wave_sync();
@@ -880,16 +885,12 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, LT&
                 if constexpr (LT::COMPACT) {
                     // intra put (idct_sse2.hpp:106-108): packus(res) -- the clamped bytes of (x, x+2)
                     uint8_t* res8 = (uint8_t*)L.res[wave] + k * RL::SIZE + RL::base(plane);
-                    const short2_t z = {0, 0}, m = {255, 255};
-    #pragma unroll
-                    for (int y = 0; y < 8; y++) {
-                        const short2_t t = __builtin_elementwise_min(__builtin_elementwise_max(s[y] >> (short)6, z), m);
-                        *(uint16_t*)&res8[(y0 + y * ys) * rw + xp] =
-                            (uint16_t)__builtin_amdgcn_perm(0u, __builtin_bit_cast(uint32_t, t), 0x0c0c0200u);
-                    }
+#pragma unroll
+                    for (int y = 0; y < 8; y++)
+                        *(uint16_t*)&res8[(y0 + y * ys) * rw + xp] = (uint16_t)sat_pk_u8(s[y] >> (short)6);
                 } else {
                     short* res = &L.res[wave][k * RL::SIZE + RL::base(plane)];
-    #pragma unroll
+#pragma unroll
                     for (int y = 0; y < 8; y++) *(short2_t*)&res[(y0 + y * ys) * rw + xp] = s[y] >> (short)6;
                 }
             }
@@ -946,13 +947,9 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, LT&
                         const int rw = RL::width(plane);
                         const int xp = RL::pos(x0 + x);
                         uint8_t* res8 = (uint8_t*)L.res[wave] + k * RL::SIZE + RL::base(plane);
-                        const short2_t z = {0, 0}, m = {255, 255};
 #pragma unroll
-                        for (int y = 0; y < 8; y++) {
-                            const short2_t tt = __builtin_elementwise_min(__builtin_elementwise_max(sv[y] >> (short)6, z), m);
-                            *(uint16_t*)&res8[(y0 + y * ys) * rw + xp] =
-                                (uint16_t)__builtin_amdgcn_perm(0u, __builtin_bit_cast(uint32_t, tt), 0x0c0c0200u);
-                        }
+                        for (int y = 0; y < 8; y++)
+                            *(uint16_t*)&res8[(y0 + y * ys) * rw + xp] = (uint16_t)sat_pk_u8(sv[y] >> (short)6);
                     }
                 }
                 wave_sync();
