@@ -613,12 +613,35 @@ __device__ __forceinline__ uint32_t dq_entry(const Group& S, int lane) {
     return (slot & 0xff) | (pick8(S.qs8, k) << 8) | (wsel << 16) | (intra << 18) | ((uint32_t)coded << 19);
 }
 
+__device__ __forceinline__ int mul24i_asm(int a, int b) {  // v_mul_i32_i24: signed 24 x 24, low 32 bits
+    int r;
+    asm("v_mul_i32_i24 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
 // dequant of one coefficient word (parse_block, mb_decoder.cpp:74-155) into its coded-block
 // slot: lane = word; its MB k (from the word's MB-column bits) and block select the group's
-// dequant entry.  INTRA_ONLY (I pictures: every MB intra, no '1s' first coefficients) drops the
-// non-intra arithmetic.
-template <class LT, bool INTRA_ONLY = false>
-__device__ __forceinline__ void dequant_word(LT& L, int wave, uint32_t w) {
+// dequant entry.  INTRA_ONLY (I pictures: every MB intra with every block coded, no '1s' first
+// coefficients) needs no table: the slot is k * NB + b, the matrix is the block's (luma for
+// blocks 0-5, mb_decoder.cpp:111-113), the quantiser scale is byte k of qs8.
+template <class LT, bool INTRA_ONLY = false, int NB = 6>
+__device__ __forceinline__ void dequant_word(LT& L, int wave, uint32_t w, uint32_t qs8) {
+    if constexpr (INTRA_ONLY) {
+        const uint32_t k = (w >> 26) & 3u, b = (w >> 22) & 15u;
+        const int slot = (int)(k * NB + b);
+        const int i = (w >> 16) & 63;
+        const int level = (short)(w & 0xffff);
+        const int Wi = L.W[b < 6 ? 0 : 2][i];
+        const uint32_t wq = __umul24((uint32_t)Wi, pick8(qs8, (int)k));
+        // (|level| * W * qs) >> 4 with the sign applied after the shift (truncation toward zero):
+        // the signed product, biased by 15 when negative, then an arithmetic shift
+        const int p = mul24i_asm(level, (int)wq);
+        const int val = (p + ((p >> 31) & 15)) >> 4;
+        short v = (short)min(max((int)(short)val, -2048), 2047);  // int16 truncation (:146), v_med3_i32
+        v = (w & MP2VG_COEF_DC) ? (short)level : v;
+        ((short*)L.blk[wave])[LT::bofs(slot, L.scan[i])] = v;
+        return;
+    }
     // the word's MB in its group: slices are whole MB rows (plan_batch), so groups start at a
     // column multiple of 4 and the MB is (column mod 8) & 3 = bits 26-27, next to the block
     // (bits 22-25): bits 22-27 index the group's dequant table.  A word's block is coded in its
@@ -793,7 +816,7 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, LT&
             // words 0..64*NCW-1 from the registers loaded one group ahead; more (rare) loaded here
 #pragma unroll
             for (int j = 0; j < NCW; j++)
-                if (64 * j + lane < S.ncoef) dequant_word<LT, MCM == 0>(L, wave, cw[j]);
+                if (64 * j + lane < S.ncoef) dequant_word<LT, MCM == 0, NB>(L, wave, cw[j], S.qs8);
             // words past the prefetch: XW loads per lane in flight per round trip, not one (a 4:4:4
             // intra group carries ~1,400 words)
             constexpr int XW = MCM == 0 ? 8 : 2;
@@ -807,7 +830,7 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, LT&
                     }
 #pragma unroll
                     for (int j = 0; j < XW; j++)
-                        if (base + 64 * j + lane < S.ncoef) dequant_word<LT, MCM == 0>(L, wave, xw[j]);
+                        if (base + 64 * j + lane < S.ncoef) dequant_word<LT, MCM == 0, NB>(L, wave, xw[j], S.qs8);
                 }
                 // Drain this rare path's loads before it rejoins: the waitcnt pass merges the
                 // paths' pending-load state, and a load it cannot prove retired (a lane-masked
