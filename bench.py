@@ -382,9 +382,13 @@ def main():
                      "traffic_write": traffic.get("write_bytes_per_step") if traffic else None,
                      "l2_requests_per_step": traffic.get("l2_requests_per_step") if traffic else None,
                      "l2_hit_rate": traffic.get("l2_hit_rate") if traffic else None,
-                     # on-chip bound: L1->L2 request bytes (64 B per request) over the algorithmic bytes
+                     # on-chip bound: L1->L2 request bytes over the algorithmic bytes, at 64 B per
+                     # request (the sector a 20-B tap row or a 64-B store quad needs) and at the
+                     # 128-B line a read request fills (tools/fetch_calib.hip): lower / upper bound
                      "l1l2_amplification": (round(traffic["l2_requests_per_step"] * 64 / alg_bytes, 3)
                                             if traffic and traffic.get("l2_requests_per_step") else None),
+                     "l1l2_amplification_128B": (round(traffic["l2_requests_per_step"] * 128 / alg_bytes, 3)
+                                                 if traffic and traffic.get("l2_requests_per_step") else None),
                      "kernel": "mp2vg::recon_kernel", "launches_per_step": len(kernel_ms[0]),
                      "avg_launch_ms": round(float(np.mean(per_launch)), 4),
                      "algorithmic_bytes_per_step": int(alg_bytes), "bytes_breakdown": parts,
