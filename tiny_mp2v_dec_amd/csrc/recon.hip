@@ -586,6 +586,18 @@ struct Lds {
     __device__ static int bofs(int slot, int idx) { return slot * BLK + (C8 ? (idx ^ ((slot & 7) << 3)) : idx); }
 };
 
+// (MB in group) * 16 + block of coded-block slot `slot`: from the group's slot map, or, in I
+// pictures (every MB intra with every block coded), slot = k * NB + b directly
+template <int MCM, int NB, class LT>
+__device__ __forceinline__ int slot_kb(const LT& L, int wave, int slot) {
+    if constexpr (MCM == 0) {
+        const int k = slot / NB;
+        return (k << 4) | (slot - k * NB);
+    } else {
+        return L.map[wave][slot];
+    }
+}
+
 struct SliceCtx {
     const uint32_t* mbrec;
     const uint32_t* coefs;
@@ -806,12 +818,12 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, LT&
 
         stamp<ABL>(st, 1);
         // ---- C. slot map + dequant (parse_block, mb_decoder.cpp:74-155) ----
-        {
+        if constexpr (MCM != 0) {  // I pictures need neither (dequant_word / slot_kb)
             const uint32_t e = dq_entry<CF>(S, lane);
             L.dq[wave][lane] = e;
             if (e & (1u << 19)) L.map[wave][e & 0xff] = (uint8_t)lane;
+            wave_sync();
         }
-        wave_sync();
         if (!(ABL & 4)) {
             // words 0..64*NCW-1 from the registers loaded one group ahead; more (rare) loaded here
 #pragma unroll
@@ -858,8 +870,8 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, LT&
                 short* const bw = (short*)L.blk[wave];
                 uint4 ra = *(const uint4*)&bw[LT::bofs(slot, v * 8)];
                 uint4 rb = *(const uint4*)&bw[LT::bofs(slot, v * 8 + 8)];
-                const int k = L.map[wave][slot] >> 4;
-                const bool intra = pick8(S.fl8, k) & MP2VG_MB_INTRA;
+                const int k = slot_kb<MCM, NB>(L, wave, slot) >> 4;
+                const bool intra = MCM == 0 || (pick8(S.fl8, k) & MP2VG_MB_INTRA);
                 uint32_t par = (ra.x ^ ra.y ^ ra.z ^ ra.w ^ rb.x ^ rb.y ^ rb.z ^ rb.w) & 0x00010001u;
                 if (v == 0 && intra) par ^= ra.x & 1u;  // DC excluded
                 par = (par ^ (par >> 16)) & 1u;
@@ -898,7 +910,7 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, LT&
                 short2_t s[8];
                 interleave(ra, rb, s);
                 idct_1d(s);
-                const int kb = L.map[wave][slot];
+                const int kb = slot_kb<MCM, NB>(L, wave, slot);
                 const int k = kb >> 4, bb = kb & 15;
                 const bool dctf = pick8(S.fl8, k) & MP2VG_MB_DCT_FIELD;
                 int plane, x0, y0, ys;
@@ -962,7 +974,7 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, LT&
 #pragma unroll
                         for (int xx = 0; xx < 8; xx++) *(short2_t*)&bw[LT::bofs(slot, xx * 8 + v)] = sv[xx];
                     } else {
-                        const int kb = L.map[wave][slot];
+                        const int kb = slot_kb<MCM, NB>(L, wave, slot);
                         const int k = kb >> 4, bb = kb & 15;
                         const bool dctf = pick8(S.fl8, k) & MP2VG_MB_DCT_FIELD;
                         int plane, x0, y0, ys;
