@@ -591,10 +591,31 @@ struct Lds {
 template <int MCM, int NB, class LT>
 __device__ __forceinline__ int slot_kb(const LT& L, int wave, int slot) {
     if constexpr (MCM == 0) {
-        const int k = slot / NB;
+        // slot / NB by a 24-bit multiply and a shift, exact for the slots of a group (< 4 * NB)
+        // (a plain division became a quarter-rate v_mul_hi_i32 + v_mad_u64_u32)
+        static_assert(NB == 6 || NB == 8 || NB == 12, "blocks per MB");
+        const int k = NB == 8 ? slot >> 3 : (int)(__umul24((uint32_t)slot, 43u) >> (NB == 6 ? 8 : 9));
         return (k << 4) | (slot - k * NB);
     } else {
         return L.map[wave][slot];
+    }
+}
+
+// IDCT pass 1's transposed writes: the 8 output pairs of lane (slot, v) go to chunk x of the
+// slot, element v.  In the compact layout chunk x sits at (x ^ (slot & 7)) * 16 bytes, so with the
+// LDS image 128-B aligned (the kernel's only __shared__ object, aligned(128); slots 128 B, wave
+// blocks multiples of 128 B) the byte address of chunk x is that of chunk 0 XOR x * 16: one v_xor
+// per write instead of an XOR and a shift-add
+typedef __attribute__((address_space(3))) short2_t lds_short2_t;
+template <class LT>
+__device__ __forceinline__ void pass1_store(short* bw, int slot, int v, const short2_t (&s)[8]) {
+    if constexpr (LT::COMPACT) {
+        const uint32_t b0 = (uint32_t)(uintptr_t)(lds_short2_t*)(bw + LT::bofs(slot, v));  // chunk 0 ^ (slot & 7)
+#pragma unroll
+        for (int x = 0; x < 8; x++) *(lds_short2_t*)(uintptr_t)(b0 ^ (uint32_t)(x << 4)) = s[x];
+    } else {
+#pragma unroll
+        for (int x = 0; x < 8; x++) *(short2_t*)&bw[LT::bofs(slot, x * 8 + v)] = s[x];
     }
 }
 
@@ -884,8 +905,7 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, LT&
                                  __builtin_bit_cast(short2_t, rb.x), __builtin_bit_cast(short2_t, rb.y),
                                  __builtin_bit_cast(short2_t, rb.z), __builtin_bit_cast(short2_t, rb.w)};
                 idct_1d(s);
-#pragma unroll
-                for (int x = 0; x < 8; x++) *(short2_t*)&bw[LT::bofs(slot, x * 8 + v)] = s[x];
+                pass1_store<LT>(bw, slot, v, s);
             }
             wave_sync();
             // chroma taps of g+1 issued mid-iteration: spreads the wave's TA demand
@@ -971,8 +991,7 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, LT&
                     }
                     idct_1d(sv);
                     if (p1) {
-#pragma unroll
-                        for (int xx = 0; xx < 8; xx++) *(short2_t*)&bw[LT::bofs(slot, xx * 8 + v)] = sv[xx];
+                        pass1_store<LT>(bw, slot, v, sv);
                     } else {
                         const int kb = slot_kb<MCM, NB>(L, wave, slot);
                         const int k = kb >> 4, bb = kb & 15;
@@ -1030,7 +1049,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MCM == 0 &&
                                                     uint8_t* __restrict__ pool, const Geo geo,
                                                     const uint32_t slice_base, const uint32_t nslices) {
     using LT = Lds<CF, MCM == 0 && ABL == 0>;
-    __shared__ __attribute__((aligned(16))) LT L;
+    __shared__ __attribute__((aligned(128))) LT L;  // 128-B aligned: pass1_store
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
