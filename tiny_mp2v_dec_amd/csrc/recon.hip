@@ -607,6 +607,12 @@ __device__ __forceinline__ int slot_kb(const LT& L, int wave, int slot) {
 // blocks multiples of 128 B) the byte address of chunk x is that of chunk 0 XOR x * 16: one v_xor
 // per write instead of an XOR and a shift-add
 typedef __attribute__((address_space(3))) short2_t lds_short2_t;
+typedef __attribute__((address_space(3))) u4v lds_uint4_t;  // (HIP's uint4 class takes no address space)
+__device__ __forceinline__ uint4 ld16(const lds_uint4_t* p) {
+    const u4v v = *p;
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void zero16(lds_uint4_t* p) { *p = u4v{0u, 0u, 0u, 0u}; }
 template <class LT>
 __device__ __forceinline__ void pass1_store(short* bw, int slot, int v, const short2_t (&s)[8]) {
     if constexpr (LT::COMPACT) {
@@ -617,6 +623,31 @@ __device__ __forceinline__ void pass1_store(short* bw, int slot, int v, const sh
 #pragma unroll
         for (int x = 0; x < 8; x++) *(short2_t*)&bw[LT::bofs(slot, x * 8 + v)] = s[x];
     }
+}
+
+// IDCT pass 2's intra put (idct_sse2.hpp:106-108, packus(res >> 6)) of columns (x, x+2) of a
+// block: row y at byte address a0 + y * step in the byte residual image.  The row step is
+// lane-varying (field DCT), so the address runs by one add per row (the row-index form cost a
+// shift-add and an add per row, and the MB offset a quarter-rate multiply)
+typedef __attribute__((address_space(3))) uint16_t lds_u16_t;
+
+// 16-B chunks ca, cb (0-7) of coded-block slot `slot` as LDS pointers, computed once for the read
+// and pass 2's zeroing (compact layout: chunk 0 XOR 16c, see pass1_store)
+template <class LT>
+__device__ __forceinline__ void slot_chunks(short* bw, int slot, int ca, int cb, lds_uint4_t*& pa, lds_uint4_t*& pb) {
+    if constexpr (LT::COMPACT) {
+        const uint32_t b0 = (uint32_t)(uintptr_t)(lds_short2_t*)(bw + LT::bofs(slot, 0));
+        pa = (lds_uint4_t*)(uintptr_t)(b0 ^ (uint32_t)(ca << 4));
+        pb = (lds_uint4_t*)(uintptr_t)(b0 ^ (uint32_t)(cb << 4));
+    } else {
+        const uint32_t b0 = (uint32_t)(uintptr_t)(lds_short2_t*)(bw + slot * LT::BLK);
+        pa = (lds_uint4_t*)(uintptr_t)(b0 + (uint32_t)(ca << 4));
+        pb = (lds_uint4_t*)(uintptr_t)(b0 + (uint32_t)(cb << 4));
+    }
+}
+__device__ __forceinline__ void put8_rows(uint32_t a0, uint32_t step, const short2_t (&s)[8]) {
+#pragma unroll
+    for (int y = 0; y < 8; y++) *(lds_u16_t*)(uintptr_t)(a0 + (uint32_t)y * step) = (uint16_t)sat_pk_u8(s[y] >> (short)6);
 }
 
 struct SliceCtx {
@@ -889,8 +920,10 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, LT&
             for (int t = lane; t < ((ABL & 1) ? 0 : S.nslots * 4); t += 64) {
                 const int slot = t >> 2, v = (t & 3) * 2;
                 short* const bw = (short*)L.blk[wave];
-                uint4 ra = *(const uint4*)&bw[LT::bofs(slot, v * 8)];
-                uint4 rb = *(const uint4*)&bw[LT::bofs(slot, v * 8 + 8)];
+                lds_uint4_t *pa, *pb;
+                slot_chunks<LT>(bw, slot, v, v + 1, pa, pb);
+                uint4 ra = ld16(pa);
+                uint4 rb = ld16(pb);
                 const int k = slot_kb<MCM, NB>(L, wave, slot) >> 4;
                 const bool intra = MCM == 0 || (pick8(S.fl8, k) & MP2VG_MB_INTRA);
                 uint32_t par = (ra.x ^ ra.y ^ ra.z ^ ra.w ^ rb.x ^ rb.y ^ rb.z ^ rb.w) & 0x00010001u;
@@ -923,10 +956,12 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, LT&
                 const int slot = t >> 2, xq = t & 3;
                 const int x = (xq & 1) | ((xq & 2) << 1);  // 0, 1, 4, 5
                 short* const bw = (short*)L.blk[wave];
-                const uint4 ra = *(const uint4*)&bw[LT::bofs(slot, x * 8)];
-                const uint4 rb = *(const uint4*)&bw[LT::bofs(slot, x * 8 + 16)];
-                *(uint4*)&bw[LT::bofs(slot, x * 8)] = make_uint4(0, 0, 0, 0);
-                *(uint4*)&bw[LT::bofs(slot, x * 8 + 16)] = make_uint4(0, 0, 0, 0);
+                lds_uint4_t *pa, *pb;
+                slot_chunks<LT>(bw, slot, x, x + 2, pa, pb);
+                const uint4 ra = ld16(pa);
+                const uint4 rb = ld16(pb);
+                zero16(pa);
+                zero16(pb);
                 short2_t s[8];
                 interleave(ra, rb, s);
                 idct_1d(s);
@@ -939,14 +974,16 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, LT&
                 const int xp = RL::pos(x0 + x);  // (x, x+2) -> (xp, xp+1)
                 if constexpr (LT::COMPACT) {
                     // intra put (idct_sse2.hpp:106-108): packus(res) -- the clamped bytes of (x, x+2)
-                    uint8_t* res8 = (uint8_t*)L.res[wave] + k * RL::SIZE + RL::base(plane);
-#pragma unroll
-                    for (int y = 0; y < 8; y++)
-                        *(uint16_t*)&res8[(y0 + y * ys) * rw + xp] = (uint16_t)sat_pk_u8(s[y] >> (short)6);
+                    const uint32_t a0 = (uint32_t)(uintptr_t)(lds_u16_t*)((uint8_t*)L.res[wave] + RL::base(plane)) +
+                                        mul24_asm((uint32_t)k, (uint32_t)RL::SIZE) + (uint32_t)(y0 * rw + xp);
+                    put8_rows(a0, (uint32_t)(ys * rw), s);
                 } else {
-                    short* res = &L.res[wave][k * RL::SIZE + RL::base(plane)];
+                    // row y at a0 + y * step, one add per row (see put8_rows)
+                    const uint32_t a0 = (uint32_t)(uintptr_t)(lds_short2_t*)(&L.res[wave][RL::base(plane)]) +
+                                        2u * (mul24_asm((uint32_t)k, (uint32_t)RL::SIZE) + (uint32_t)(y0 * rw + xp));
+                    const uint32_t step = 2u * (uint32_t)(ys * rw);
 #pragma unroll
-                    for (int y = 0; y < 8; y++) *(short2_t*)&res[(y0 + y * ys) * rw + xp] = s[y] >> (short)6;
+                    for (int y = 0; y < 8; y++) *(lds_short2_t*)(uintptr_t)(a0 + (uint32_t)y * step) = s[y] >> (short)6;
                 }
             }
             wave_sync();
@@ -969,8 +1006,12 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, LT&
                     const int slot = u >> 2, q = u & 3;
                     const int v = q * 2;                           // pass 1: rows v, v+1
                     const int x = (q & 1) | ((q & 2) << 1);       // pass 2: columns x, x+2 (0, 1, 4, 5)
-                    uint4 ra = *(const uint4*)&bw[LT::bofs(slot, p1 ? v * 8 : x * 8)];
-                    uint4 rb = *(const uint4*)&bw[LT::bofs(slot, p1 ? v * 8 + 8 : x * 8 + 16)];
+                    // the item's two 16-B chunks (pass 1: rows v, v+1; pass 2: columns x, x+2); pass 2
+                    // zeroes them after reading
+                    lds_uint4_t *pa, *pb;
+                    slot_chunks<LT>(bw, slot, p1 ? v : x, p1 ? v + 1 : x + 2, pa, pb);
+                    uint4 ra = ld16(pa);
+                    uint4 rb = ld16(pb);
                     short2_t sv[8];
                     if (p1) {
                         // mismatch control (intra: DC excluded), as in pass 1 above
@@ -985,8 +1026,8 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, LT&
                         sv[4] = __builtin_bit_cast(short2_t, rb.x), sv[5] = __builtin_bit_cast(short2_t, rb.y);
                         sv[6] = __builtin_bit_cast(short2_t, rb.z), sv[7] = __builtin_bit_cast(short2_t, rb.w);
                     } else {
-                        *(uint4*)&bw[LT::bofs(slot, x * 8)] = make_uint4(0, 0, 0, 0);
-                        *(uint4*)&bw[LT::bofs(slot, x * 8 + 16)] = make_uint4(0, 0, 0, 0);
+                        zero16(pa);
+                        zero16(pb);
                         interleave(ra, rb, sv);
                     }
                     idct_1d(sv);
@@ -1000,10 +1041,9 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, LT&
                         block_origin<CF>(bb, dctf, plane, x0, y0, ys);
                         const int rw = RL::width(plane);
                         const int xp = RL::pos(x0 + x);
-                        uint8_t* res8 = (uint8_t*)L.res[wave] + k * RL::SIZE + RL::base(plane);
-#pragma unroll
-                        for (int y = 0; y < 8; y++)
-                            *(uint16_t*)&res8[(y0 + y * ys) * rw + xp] = (uint16_t)sat_pk_u8(sv[y] >> (short)6);
+                        const uint32_t a0 = (uint32_t)(uintptr_t)(lds_u16_t*)((uint8_t*)L.res[wave] + RL::base(plane)) +
+                                            mul24_asm((uint32_t)k, (uint32_t)RL::SIZE) + (uint32_t)(y0 * rw + xp);
+                        put8_rows(a0, (uint32_t)(ys * rw), sv);
                     }
                 }
                 wave_sync();
