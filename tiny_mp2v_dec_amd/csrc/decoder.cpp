@@ -27,6 +27,7 @@
 #include <thread>
 #include <vector>
 
+#include "recon_kernel.h"
 #include "syntax.h"
 
 using namespace mp2vg;
@@ -47,6 +48,10 @@ const int kChunk = getenv("MP2VG_CHUNK") ? std::max(1, atoi(getenv("MP2VG_CHUNK"
 // 7,451-7,488; MP2VG_DL_STREAMS overrides it for measurements)
 constexpr int kMaxDl = 4;
 const int kDlStreams = getenv("MP2VG_DL_STREAMS") ? std::min(kMaxDl, std::max(1, atoi(getenv("MP2VG_DL_STREAMS")))) : 4;
+// host frames come back by one copy kernel launch per chunk (recon.hip frame_copy_kernel, stores
+// over PCIe into the pinned frames) instead of one DMA per frame; MP2VG_DL_KERNEL=0 selects the
+// DMA copies (measurements)
+const bool kDlKernel = !getenv("MP2VG_DL_KERNEL") || atoi(getenv("MP2VG_DL_KERNEL")) != 0;
 
 // Host frames live in pinned memory, in the device slot layout (= the reference frame_c layout),
 // so a decoded slot comes back with one contiguous DMA copy (with MP2VG_DECODER_DEVICE_FRAMES
@@ -535,6 +540,16 @@ extern "C" int mp2vg_decoder_decode(mp2vg_decoder_t* d, const uint8_t* buf, uint
         for (int i = 0; i < L.ndl; i++)
             if (hipStreamWaitEvent(L.dl[i], L.decoded, 0) != hipSuccess) return MP2VG_E_HIP;
         FramePool& pool = d->device_frames ? *L.dpool : *d->hpool;
+        FrameCopy fc;
+        int nfc = 0;
+        auto flush_copies = [&]() -> int {
+            if (nfc && launch_frame_copy(fc, nfc, d->g.slot_bytes, L.dl[0]) != hipSuccess) {
+                set_error("frame copy kernel launch failed");
+                return MP2VG_E_HIP;
+            }
+            nfc = 0;
+            return MP2VG_OK;
+        };
         for (int p = s; p < e; p++) {
             HostFrame* hf = pool.get(renderer_holds);
             if (!hf) return MP2VG_E_NOMEM;
@@ -550,6 +565,19 @@ extern "C" int mp2vg_decoder_decode(mp2vg_decoder_t* d, const uint8_t* buf, uint
             void* src = nullptr;
             rc = mp2vg_slot_device_ptr(L.ctx, slot_of[p], &src);
             hipSetDevice(L.device);
+            // the pinned frame as this device addresses it (a frame the device cannot map goes
+            // by DMA)
+            void* hdst = nullptr;
+            const bool by_kernel = kDlKernel && !d->device_frames &&
+                                   hipHostGetDevicePointer(&hdst, hf->data, 0) == hipSuccess &&
+                                   !(((uintptr_t)hdst | (uintptr_t)src) & 15);
+            if (rc == MP2VG_OK && by_kernel) {
+                fc.src[nfc] = (const uint8_t*)src;
+                fc.dst[nfc++] = (uint8_t*)hdst;
+                L.inflight[p] = hf;
+                if (nfc == kFrameCopyMax && (rc = flush_copies()) != MP2VG_OK) return rc;
+                continue;
+            }
             if (rc == MP2VG_OK && hipMemcpyAsync(hf->data, src, d->g.slot_bytes,
                                                  d->device_frames ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost,
                                                  L.dl[p % L.ndl]) != hipSuccess)
@@ -560,6 +588,7 @@ extern "C" int mp2vg_decoder_decode(mp2vg_decoder_t* d, const uint8_t* buf, uint
             }
             L.inflight[p] = hf;
         }
+        if ((rc = flush_copies()) != MP2VG_OK) return rc;
         L.pend.clear();
         for (int p = s; p < e; p++) L.pend.push_back(p);
         return MP2VG_OK;

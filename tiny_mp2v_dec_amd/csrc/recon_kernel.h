@@ -64,4 +64,13 @@ struct KArgs {
     uint32_t nslices;
 };
 
+// decoded slots -> host (or HBM) frames of one drop-in chunk, by a copy kernel (recon.hip);
+// 16-B aligned pointers, kernel arguments by value
+constexpr int kFrameCopyMax = 32;
+struct FrameCopy {
+    const uint8_t* src[kFrameCopyMax];
+    uint8_t* dst[kFrameCopyMax];
+};
+hipError_t launch_frame_copy(const FrameCopy& fc, int n, uint64_t bytes, hipStream_t stream);
+
 }  // namespace mp2vg
