@@ -35,11 +35,14 @@ def test_dropin_python_api(entry):
     assert threading.get_ident() not in threads  # callbacks ran on the render thread
 
 
-def test_dropin_cpp_cli_matches_reference(tmp_path):
+@pytest.mark.parametrize("dl_kernel", ["1", "0"], ids=["copy_kernel", "dma"])
+def test_dropin_cpp_cli_matches_reference(tmp_path, dl_kernel):
+    """Frames come back by the copy kernel (default) or, with MP2VG_DL_KERNEL=0, one DMA per frame."""
     e = next(m for m in MANIFEST if m["name"] == "hd1080_420_ipb")
     out = tmp_path / "o.yuv"
     r = subprocess.run([B.CLI, "-v", os.path.join(STREAMS, e["file"]), "-o", str(out), "-w", "1920", "-h", "1088",
-                        "-c", "1"], capture_output=True, text=True, timeout=300)
+                        "-c", "1"], capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, MP2VG_DL_KERNEL=dl_kernel))
     assert r.returncode == 0, r.stderr
     assert "Time =" in r.stdout
     data = out.read_bytes()

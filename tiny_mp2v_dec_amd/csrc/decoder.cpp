@@ -207,6 +207,9 @@ struct mp2vg_decoder {
     std::vector<std::unique_ptr<Lane>> lanes;
     std::unique_ptr<FramePool> hpool;  // pinned host frames, shared by every lane
     bool device_frames = false;        // MP2VG_DECODER_DEVICE_FRAMES: frames handed over in HBM
+    // host frames by the copy kernel: every lane on one device (the pinned pool is mapped for the
+    // device it was allocated under; lanes on several devices copy by DMA)
+    bool kernel_copy = false;
     mp2vg_stream_headers_t hdrs{};     // of the last decode()
 };
 
@@ -234,6 +237,8 @@ extern "C" int mp2vg_decoder_create_multi(const mp2vg_config_t* cfg, const int32
     d->user = user;
     d->g.init(cfg->width, cfg->height, cfg->chroma_format);
     d->device_frames = cfg->reserved & MP2VG_DECODER_DEVICE_FRAMES;
+    d->kernel_copy = kDlKernel && !d->device_frames;
+    for (int i = 1; i < ndevices; i++) d->kernel_copy = d->kernel_copy && devices[i] == devices[0];
     // frames in flight per lane: one chunk being copied, one being rendered, anchors held for display
     const int frames_per_lane = 2 * kChunk + 4;
     const size_t chunk_mbs = (size_t)kChunk * (cfg->width / 16) * (cfg->height / 16);
@@ -568,7 +573,7 @@ extern "C" int mp2vg_decoder_decode(mp2vg_decoder_t* d, const uint8_t* buf, uint
             // the pinned frame as this device addresses it (a frame the device cannot map goes
             // by DMA)
             void* hdst = nullptr;
-            const bool by_kernel = kDlKernel && !d->device_frames &&
+            const bool by_kernel = d->kernel_copy &&
                                    hipHostGetDevicePointer(&hdst, hf->data, 0) == hipSuccess &&
                                    !(((uintptr_t)hdst | (uintptr_t)src) & 15);
             if (rc == MP2VG_OK && by_kernel) {
