@@ -44,14 +44,22 @@ __device__ __forceinline__ short2_t mulhi2_x2(short2_t a, int c) {
     return __builtin_bit_cast(short2_t, __builtin_bit_cast(uint32_t, h) & 0xfffefffeu);
 }
 
-// idct_sse2.hpp:23-65, two lanes of the SSE2 vector at once
+// idct_sse2.hpp:23-65, two lanes of the SSE2 vector at once.
+// P1: the first pass over dequantised coefficients.  Every input but QFS[0] (s[0] of the rows-0/1
+// item: the intra DC or the unclamped '1s' coefficient) is clamped to [-2048, 2047] by dequant
+// (mb_decoder.cpp:146; mismatch control only flips bit 0 of QFS[63]), and for |a| <= 8191
+//   adds(mulhi(a, c), slli(a, n)) = floor(a * (c + 2^(16+n)) / 2^16)   (no wrap, no saturation)
+//   adds(slli(mulhi(a, c), 1), slli(a, n)) = 2 * floor(a * (c + 2^(15+n)) / 2^16)
+// so the first-stage terms of s[1..5] are one mulhi each (two products and a perm) instead of a
+// mulhi, a packed shift and a saturating packed add.  s[0] keeps the exact form.
+template <bool P1 = false>
 __device__ __forceinline__ void idct_1d(short2_t s[8]) {
     const short2_t v15 = adds2(mulhi2_x2(s[0], 27145), shl2(s[0], 1));
-    const short2_t v26 = adds2(mulhi2(s[1], -5037), shl2(s[1], 2));
-    const short2_t v21 = adds2(mulhi2(s[2], -19954), shl2(s[2], 2));
-    const short2_t v28 = adds2(mulhi2_x2(s[3], -22089), shl2(s[3], 2));
-    const short2_t v16 = adds2(mulhi2_x2(s[4], 27145), shl2(s[4], 1));
-    const short2_t v25 = adds2(mulhi2(s[5], 14567), shl2(s[5], 1));
+    const short2_t v26 = P1 ? mulhi2(s[1], -5037 + 262144) : adds2(mulhi2(s[1], -5037), shl2(s[1], 2));
+    const short2_t v21 = P1 ? mulhi2(s[2], -19954 + 262144) : adds2(mulhi2(s[2], -19954), shl2(s[2], 2));
+    const short2_t v28 = P1 ? mulhi2_x2(s[3], -22089 + 131072) : adds2(mulhi2_x2(s[3], -22089), shl2(s[3], 2));
+    const short2_t v16 = P1 ? mulhi2_x2(s[4], 27145 + 65536) : adds2(mulhi2_x2(s[4], 27145), shl2(s[4], 1));
+    const short2_t v25 = P1 ? mulhi2(s[5], 14567 + 131072) : adds2(mulhi2(s[5], 14567), shl2(s[5], 1));
     const short2_t v22 = adds2(mulhi2_x2(s[6], 17391), s[6]);
     const short2_t v27 = mulhi2_x2(s[7], 25570);
     const short2_t v19 = subs2(v25, v28);
@@ -937,7 +945,7 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, LT&
                                  __builtin_bit_cast(short2_t, ra.z), __builtin_bit_cast(short2_t, ra.w),
                                  __builtin_bit_cast(short2_t, rb.x), __builtin_bit_cast(short2_t, rb.y),
                                  __builtin_bit_cast(short2_t, rb.z), __builtin_bit_cast(short2_t, rb.w)};
-                idct_1d(s);
+                idct_1d<true>(s);
                 pass1_store<LT>(bw, slot, v, s);
             }
             wave_sync();
@@ -1030,7 +1038,10 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, LT&
                         zero16(pb);
                         interleave(ra, rb, sv);
                     }
-                    idct_1d(sv);
+                    if (base + 64 <= n4)
+                        idct_1d<true>(sv);
+                    else
+                        idct_1d(sv);
                     if (p1) {
                         pass1_store<LT>(bw, slot, v, sv);
                     } else {
