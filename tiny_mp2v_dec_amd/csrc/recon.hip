@@ -51,7 +51,8 @@ __device__ __forceinline__ short2_t mulhi2_x2(short2_t a, int c) {
 //   adds(mulhi(a, c), slli(a, n)) = floor(a * (c + 2^(16+n)) / 2^16)   (no wrap, no saturation)
 //   adds(slli(mulhi(a, c), 1), slli(a, n)) = 2 * floor(a * (c + 2^(15+n)) / 2^16)
 // so the first-stage terms of s[1..5] are one mulhi each (two products and a perm) instead of a
-// mulhi, a packed shift and a saturating packed add.  s[0] keeps the exact form.
+// mulhi, a packed shift and a saturating packed add.  s[0] keeps the exact form.  The bounds and
+// the whole folded transform are checked against the exact one in tests/test_idct_fold.py.
 template <bool P1 = false>
 __device__ __forceinline__ void idct_1d(short2_t s[8]) {
     const short2_t v15 = adds2(mulhi2_x2(s[0], 27145), shl2(s[0], 1));
@@ -73,12 +74,14 @@ __device__ __forceinline__ void idct_1d(short2_t s[8]) {
     const short2_t v8 = adds2(v15, v16);
     const short2_t v9 = subs2(v15, v16);
     const short2_t v18 = mulhi2(subs2(v19, v20), 25079);              // op4
-    const short2_t v12 = subs2(v18, adds2(v19, mulhi2(v19, 20090)));  // op3
+    // op3, op0: a + mulhi(a, c) = mulhi(a, c + 2^16) in pass 1 (|v19| <= 11,363, |v13| <= 20,998,
+    // |v17| <= 10,703 there: no saturation, products below 2^31)
+    const short2_t v12 = subs2(v18, P1 ? mulhi2(v19, 20090 + 65536) : adds2(v19, mulhi2(v19, 20090)));  // op3
     const short2_t v14 = subs2(subs2(v20, mulhi2(v20, 30068)), v18);  // op1
     const short2_t v6 = subs2(shl2(v14, 1), v7);
-    const short2_t v5 = subs2(adds2(v13, mulhi2(v13, 27145)), v6);    // op0
+    const short2_t v5 = subs2(P1 ? mulhi2(v13, 27145 + 65536) : adds2(v13, mulhi2(v13, 27145)), v6);    // op0
     const short2_t v4 = adds2(v5, shl2(v12, 1));
-    const short2_t v10 = subs2(adds2(v17, mulhi2(v17, 27145)), v11);  // op0
+    const short2_t v10 = subs2(P1 ? mulhi2(v17, 27145 + 65536) : adds2(v17, mulhi2(v17, 27145)), v11);  // op0
     const short2_t v0 = adds2(v8, v11);
     const short2_t v1 = adds2(v9, v10);
     const short2_t v2 = subs2(v9, v10);
