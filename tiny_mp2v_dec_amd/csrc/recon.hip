@@ -700,7 +700,7 @@ __device__ __forceinline__ int mul24i_asm(int a, int b) {  // v_mul_i32_i24: sig
 // coefficients) needs no table: the slot is k * NB + b, the matrix is the block's (luma for
 // blocks 0-5, mb_decoder.cpp:111-113), the quantiser scale is byte k of qs8.
 template <class LT, bool INTRA_ONLY = false, int NB = 6>
-__device__ __forceinline__ void dequant_word(LT& L, int wave, uint32_t w, uint32_t qs8) {
+__device__ __forceinline__ void dequant_word(LT& L, int wave, uint32_t w, uint32_t qs8, bool live = true) {
     if constexpr (INTRA_ONLY) {
         const uint32_t k = (w >> 26) & 3u, b = (w >> 22) & 15u;
         const int slot = (int)(k * NB + b);
@@ -714,7 +714,10 @@ __device__ __forceinline__ void dequant_word(LT& L, int wave, uint32_t w, uint32
         const int val = (p + ((p >> 31) & 15)) >> 4;
         short v = (short)min(max((int)(short)val, -2048), 2047);  // int16 truncation (:146), v_med3_i32
         v = (w & MP2VG_COEF_DC) ? (short)level : v;
-        ((short*)L.blk[wave])[LT::bofs(slot, L.scan[i])] = v;
+        // a lane past the group's words writes its (meaningless) value to byte 0 of the wave's
+        // residual image instead, which IDCT pass 2 rewrites before the store pass reads it
+        short* const dst = live ? &((short*)L.blk[wave])[LT::bofs(slot, L.scan[i])] : (short*)L.res[wave];
+        *dst = v;
         return;
     }
     // the word's MB in its group: slices are whole MB rows (plan_batch), so groups start at a
@@ -889,9 +892,19 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, LT&
         }
         if (!(ABL & 4)) {
             // words 0..64*NCW-1 from the registers loaded one group ahead; more (rare) loaded here
+            if constexpr (MCM == 0) {
+                // I pictures: registers up to the group's last word, lanes past it masked by their
+                // store address rather than by exec (no divergent branch per word register)
 #pragma unroll
-            for (int j = 0; j < NCW; j++)
-                if (64 * j + lane < S.ncoef) dequant_word<LT, MCM == 0, NB>(L, wave, cw[j], S.qs8);
+                for (int j = 0; j < NCW; j++) {
+                    if (64 * j >= S.ncoef) break;
+                    dequant_word<LT, true, NB>(L, wave, cw[j], S.qs8, 64 * j + lane < S.ncoef);
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < NCW; j++)
+                    if (64 * j + lane < S.ncoef) dequant_word<LT, false, NB>(L, wave, cw[j], S.qs8);
+            }
             // words past the prefetch: XW loads per lane in flight per round trip, not one (a 4:4:4
             // intra group carries ~1,400 words)
             constexpr int XW = MCM == 0 ? 8 : 2;
