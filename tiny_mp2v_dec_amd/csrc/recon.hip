@@ -592,6 +592,11 @@ struct Lds {
     uint8_t map[WAVES][MAXS];                    // slot -> k*16 + b
     uint32_t dq[WAVES][64];                      // (k*16 + b) -> dequant parameters (DqEntry)
     uint8_t W[4][64];
+    // 4:2:0 / 4:2:2 I kernels (WB): the intra matrix row of each block b (W[0] for b < 6, W[2]
+    // above), so a coefficient word's (b, i) bits 16-25 index it directly; scan positions stored
+    // doubled (byte offsets of an int16 in the block).  4:4:4 measured 1 % slower with it.
+    static constexpr bool WB = C8 && CF != 3;
+    uint8_t Wb[WB ? Fmt<CF>::NB : 0][64];  // zero-length (clang extension) when unused: no layout change
     uint8_t scan[64];
     // short index of coefficient / pass-1 output idx (0..63) of a slot, relative to the wave's blk
     __device__ static int bofs(int slot, int idx) { return slot * BLK + (C8 ? (idx ^ ((slot & 7) << 3)) : idx); }
@@ -706,18 +711,32 @@ __device__ __forceinline__ void dequant_word(LT& L, int wave, uint32_t w, uint32
         const int slot = (int)(k * NB + b);
         const int i = (w >> 16) & 63;
         const int level = (short)(w & 0xffff);
-        const int Wi = L.W[b < 6 ? 0 : 2][i];
+        const int Wi = LT::WB ? ((const uint8_t*)L.Wb)[(w >> 16) & 0x3ffu] : L.W[b < 6 ? 0 : 2][i];
         const uint32_t wq = __umul24((uint32_t)Wi, pick8(qs8, (int)k));
         // (|level| * W * qs) >> 4 with the sign applied after the shift (truncation toward zero):
         // the signed product, biased by 15 when negative, then an arithmetic shift
         const int p = mul24i_asm(level, (int)wq);
         const int val = (p + ((p >> 31) & 15)) >> 4;
-        short v = (short)min(max((int)(short)val, -2048), 2047);  // int16 truncation (:146), v_med3_i32
-        v = (w & MP2VG_COEF_DC) ? (short)level : v;
+        const int v = min(max((int)(short)val, -2048), 2047);  // int16 truncation (:146), v_med3_i32
+        short o;
+        if constexpr (LT::WB) {
+            const int dcm = (int)(w << 1) >> 31;  // DC word (bit 30): the value itself
+            o = (short)((level & dcm) | (v & ~dcm));
+        } else {
+            o = (w & MP2VG_COEF_DC) ? (short)level : (short)v;
+        }
         // a lane past the group's words writes its (meaningless) value to byte 0 of the wave's
         // residual image instead, which IDCT pass 2 rewrites before the store pass reads it
-        short* const dst = live ? &((short*)L.blk[wave])[LT::bofs(slot, L.scan[i])] : (short*)L.res[wave];
-        *dst = v;
+        if constexpr (LT::WB) {
+            // byte address: slot * 128 + ((slot & 7) * 16 XOR doubled scan position)
+            const uint32_t a = (uint32_t)(uintptr_t)(lds_short2_t*)L.blk[wave] + ((uint32_t)slot << 7) +
+                               ((((uint32_t)slot << 4) & 0x70u) ^ (uint32_t)L.scan[i]);
+            const uint32_t d = (uint32_t)(uintptr_t)(lds_short2_t*)L.res[wave];
+            *(__attribute__((address_space(3))) short*)(uintptr_t)(live ? a : d) = o;
+        } else {
+            short* const dst = live ? &((short*)L.blk[wave])[LT::bofs(slot, L.scan[i])] : (short*)L.res[wave];
+            *dst = o;
+        }
         return;
     }
     // the word's MB in its group: slices are whole MB rows (plan_batch), so groups start at a
@@ -1132,7 +1151,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MCM == 0 &&
         // blocks sit in LDS pair-interleaved: coefficient (v, u) at (v >> 1) * 16 + u * 2 + (v & 1),
         // so a dword is the (row v, row v + 1) pair of column u that IDCT pass 1 transforms
         const int r = c_scan_raster[alt][tid];
-        L.scan[tid] = (uint8_t)((r >> 4) * 16 + (r & 7) * 2 + ((r >> 3) & 1));
+        const int pos = (r >> 4) * 16 + (r & 7) * 2 + ((r >> 3) & 1);
+        L.scan[tid] = (uint8_t)(LT::WB ? 2 * pos : pos);
+        if constexpr (LT::WB) {
+#pragma unroll
+            for (int bb = 0; bb < Fmt<CF>::NB; bb++) L.Wb[bb][tid] = pic->W[bb < 6 ? 0 : 2][tid];
+        }
     }
     for (int i = lane; i < LT::MAXS * LT::BLK / 2; i += 64) ((uint32_t*)L.blk[wave])[i] = 0;
     __syncthreads();
