@@ -592,12 +592,13 @@ struct Lds {
     uint8_t map[WAVES][MAXS];                    // slot -> k*16 + b
     uint32_t dq[WAVES][64];                      // (k*16 + b) -> dequant parameters (DqEntry)
     uint8_t W[4][64];
-    // 4:2:0 / 4:2:2 I kernels (WB): the intra matrix row of each block b (W[0] for b < 6, W[2]
-    // above), so a coefficient word's (b, i) bits 16-25 index it directly; scan positions stored
-    // doubled (byte offsets of an int16 in the block).  4:4:4 measured 1 % slower with it.
-    static constexpr bool WB = C8 && CF != 3;
-    uint8_t Wb[WB ? Fmt<CF>::NB : 0][64];  // zero-length (clang extension) when unused: no layout change
+    // I kernels (WB): the intra matrix row of each block b (W[0] for b < 6, W[2] above), so a
+    // coefficient word's (b, i) bits 16-25 index it directly; scan positions stored doubled (byte
+    // offsets of an int16 in the block).  The table sits after `scan`: c5 is sensitive to where
+    // the small tables sit (scan 64 B further on: -5 %; the table in front of scan: -1 %)
+    static constexpr bool WB = C8;
     uint8_t scan[64];
+    uint8_t Wb[WB ? Fmt<CF>::NB : 0][64];  // zero-length (clang extension) when unused: no layout change
     // short index of coefficient / pass-1 output idx (0..63) of a slot, relative to the wave's blk
     __device__ static int bofs(int slot, int idx) { return slot * BLK + (C8 ? (idx ^ ((slot & 7) << 3)) : idx); }
 };
