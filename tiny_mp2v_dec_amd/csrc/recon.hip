@@ -598,7 +598,7 @@ struct Lds {
     // the small tables sit (scan 64 B further on: -5 %; the table in front of scan: -1 %)
     static constexpr bool WB = C8;
     uint8_t scan[64];
-    uint8_t Wb[WB ? Fmt<CF>::NB : 0][64];  // zero-length (clang extension) when unused: no layout change
+    uint8_t Wb[WB && CF != 1 ? Fmt<CF>::NB : 0][64];  // zero-length (clang extension) when unused: no layout change
     // short index of coefficient / pass-1 output idx (0..63) of a slot, relative to the wave's blk
     __device__ static int bofs(int slot, int idx) { return slot * BLK + (C8 ? (idx ^ ((slot & 7) << 3)) : idx); }
 };
@@ -712,7 +712,10 @@ __device__ __forceinline__ void dequant_word(LT& L, int wave, uint32_t w, uint32
         const int slot = (int)(k * NB + b);
         const int i = (w >> 16) & 63;
         const int level = (short)(w & 0xffff);
-        const int Wi = LT::WB ? ((const uint8_t*)L.Wb)[(w >> 16) & 0x3ffu] : L.W[b < 6 ? 0 : 2][i];
+        // 4:2:0: every block uses the luma intra matrix (blocks 4/5 too, mb_decoder.cpp:184-185),
+        // so W[0][i] directly: one 64-B table, no bank conflicts between block rows
+        const int Wi = NB == 6 ? L.W[0][i]
+                               : (LT::WB ? ((const uint8_t*)L.Wb)[(w >> 16) & 0x3ffu] : L.W[b < 6 ? 0 : 2][i]);
         const uint32_t wq = __umul24((uint32_t)Wi, pick8(qs8, (int)k));
         // (|level| * W * qs) >> 4 with the sign applied after the shift (truncation toward zero):
         // the signed product, biased by 15 when negative, then an arithmetic shift
@@ -1154,7 +1157,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MCM == 0 &&
         const int r = c_scan_raster[alt][tid];
         const int pos = (r >> 4) * 16 + (r & 7) * 2 + ((r >> 3) & 1);
         L.scan[tid] = (uint8_t)(LT::WB ? 2 * pos : pos);
-        if constexpr (LT::WB) {
+        if constexpr (LT::WB && CF != 1) {
 #pragma unroll
             for (int bb = 0; bb < Fmt<CF>::NB; bb++) L.Wb[bb][tid] = pic->W[bb < 6 ? 0 : 2][tid];
         }
