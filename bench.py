@@ -42,8 +42,10 @@ CONFIGS = {
 }
 
 
-# GOPs per GPU per step (c1, c5: I-only, one picture per "GOP"; c4: 4K, 192 frames = 2.4 GB per step)
-DEFAULT_GOPS = {"c1": 120, "c2": 64, "c3": 64, "c4": 16, "c5": 64}
+# GOPs per GPU per step (c1, c5: I-only, one picture per "GOP"; c4: 4K, 192 frames = 2.4 GB per step;
+# c2: 3,072 frames = 9.6 GB of frames per step -- level launches 4x longer than at 64 GOPs, so their
+# ramps and tails are amortised: 337.5k vs 328.3k frames/s, profiles/r3/README.md)
+DEFAULT_GOPS = {"c1": 120, "c2": 256, "c3": 64, "c4": 16, "c5": 64}
 
 
 def algorithmic_bytes(parsed):
