@@ -42,10 +42,12 @@ CONFIGS = {
 }
 
 
-# GOPs per GPU per step (c1, c5: I-only, one picture per "GOP"; c4: 4K, 192 frames = 2.4 GB per step;
-# c2: 3,072 frames = 9.6 GB of frames per step -- level launches 4x longer than at 64 GOPs, so their
-# ramps and tails are amortised: 337.5k vs 328.3k frames/s, profiles/r3/README.md)
-DEFAULT_GOPS = {"c1": 120, "c2": 256, "c3": 64, "c4": 16, "c5": 64}
+# GOPs per GPU per step (c1, c5: I-only, one picture per "GOP").  The IPB configs keep ~10 GB of
+# frames resident per step (c2: 3,072 frames = 9.6 GB; c3: 3,072 frames = 12.8 GB; c4: 4K, 768 frames =
+# 9.5 GB): level launches 4x longer than at the earlier 64 / 64 / 16 GOPs amortise their ramps and
+# tails (same box: c2 337.5k vs 328.3k, c3 256.0k vs 234.6k, c4 89.0k vs 83.1k frames/s;
+# profiles/r3/README.md)
+DEFAULT_GOPS = {"c1": 120, "c2": 256, "c3": 256, "c4": 64, "c5": 64}
 
 
 def algorithmic_bytes(parsed):
