@@ -23,6 +23,38 @@ import numpy as np
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks_if_needed(argv):
+    """`python bench.py --gpus N` with N > 1 outside a torch.distributed launcher: run the N ranks
+    (one process per GPU) as ONE child, `python -m torch.distributed.run --nproc-per-node N`, on
+    127.0.0.1, forward its output and exit with its status.  This process never imports torch
+    and never touches a GPU (an exec from a GPU-initialised process is forbidden on this pool).
+    Under a launcher (WORLD_SIZE set) nothing happens here and main() checks world == --gpus."""
+    if "WORLD_SIZE" in os.environ:
+        return
+    ap = argparse.ArgumentParser(add_help=False)
+    ap.add_argument("--gpus", type=int, default=1)
+    known, _ = ap.parse_known_args(argv)
+    if known.gpus <= 1:
+        return
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={known.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + list(argv)
+    sys.stdout.flush()
+    sys.exit(subprocess.run(cmd).returncode)
+
+
+if __name__ == "__main__":
+    spawn_ranks_if_needed(sys.argv[1:])
+
 from tiny_mp2v_dec_amd import build as _build  # noqa: E402
 from tiny_mp2v_dec_amd import records as R  # noqa: E402
 
@@ -162,7 +194,9 @@ def init_distributed(backend):
     ndev = max(1, torch.cuda.device_count())  # does not initialise the GPU
     device = local_rank % ndev
     dist, coll_dev = None, "cpu"
-    if world > 1:
+    # under a launcher the process group is formed even at world 1 (a one-rank RCCL run executes
+    # every collective of the N-GPU path on one MI355X: tests/test_bench_multirank.py)
+    if "WORLD_SIZE" in os.environ:
         import torch.distributed as tdist
         if backend == "nccl":
             torch.cuda.set_device(device)
@@ -259,9 +293,24 @@ def main():
                     help="GOPs per rank in the rank-0 frame gather measured after the timed region")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the drop-in end-to-end measurement")
+    ap.add_argument("--probe-launch", action="store_true",
+                    help="form the process group, check world == --gpus with one all_reduce, print one JSON "
+                         "line and exit before any GPU work (CPU test of the N-rank launch)")
     args = ap.parse_args()
 
     rank, world, dist, coll_dev, device = init_distributed(args.backend)
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started {world} rank(s)")
+    if args.probe_launch:
+        from tiny_mp2v_dec_amd import gather as G
+        ranks = G.gather_u64(np.array([rank], np.uint64), dist, coll_dev)
+        mx = G.max_over_ranks(rank, dist, coll_dev)
+        if rank == 0:
+            print(json.dumps({"probe": "launch", "n_gpus": world, "backend": args.backend if dist else None,
+                              "ranks": [int(r[0]) for r in ranks], "max_rank": mx}), flush=True)
+        if dist is not None:
+            dist.destroy_process_group()
+        return
     import torch
 
     if rank == 0:
@@ -377,7 +426,7 @@ def main():
         "config": {"workload": f"{desc}, pre-parsed MB records resident in HBM, {gops} GOPs per GPU",
                    "width": width, "height": height, "chroma_format": {1: "4:2:0", 2: "4:2:2", 3: "4:4:4"}[cf],
                    "frames_per_gpu_per_step": parsed.npics, "global_batch_frames": parsed.npics * world,
-                   "parallelism": f"gop-shard x{world}", "backend": args.backend if world > 1 else None},
+                   "parallelism": f"gop-shard x{world}", "backend": args.backend if dist is not None else None},
         "parity": parity,
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic["traffic_bytes_per_step"] if traffic else None,
@@ -407,9 +456,9 @@ def main():
     if gather_res is not None:
         result["frame_gather"] = gather_res
     ctx.close()
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and dist is None and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(es, width, height, cf, parsed.npics)
-    if rank == 0 and world == 1 and not args.no_e2e:
+    if rank == 0 and world == 1 and dist is None and not args.no_e2e:
         result["e2e_dropin"] = e2e_dropin(es, width, height, cf, parsed.npics, device,
                                           result.get("cpu_baseline"))
     if rank == 0:

@@ -31,7 +31,9 @@ static void write_yuv(FILE* fp, frame_c* frame) {
 
 // Per-frame 64-bit digest of the visible planes, the host twin of the device digest
 // (tiny_mp2v_dec_amd.records.planes_digest): sum over visible little-endian dwords d at
-// (row_id, byte x), rows numbered across Y, U, V, of mix64((row_id << 32) | x) ^ d, mod 2^64.
+// (row_id, byte x), rows numbered across Y, U, V, of mix64(mix64((row_id << 32) | x) ^ d), mod
+// 2^64.  Mixing after the dword is combined makes every term a pseudo-random function of its
+// value: paired small errors (two +-1 pixels in one byte lane) cannot cancel in the sum.
 static uint64_t mix64(uint64_t z) {
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
@@ -46,7 +48,7 @@ static uint64_t frame_digest(frame_c* frame) {
             for (int x = 0; x + 4 <= frame->get_width(i); x += 4) {
                 uint32_t d;
                 memcpy(&d, plane + x, 4);
-                acc += mix64((row_id << 32) | (uint64_t)x) ^ (uint64_t)d;
+                acc += mix64(mix64((row_id << 32) | (uint64_t)x) ^ (uint64_t)d);
             }
     }
     return acc;

@@ -55,7 +55,8 @@ def main():
     only = set(sys.argv[1:])  # e.g. "c1": (re)compute only these configs, keep the other keys
     out = {}
     path = os.path.join(HERE, "bench_digests.npz")
-    if only and os.path.exists(path):
+    resume = bool(os.environ.get("MP2VG_DIGESTS_RESUME"))
+    if (only or resume) and os.path.exists(path):
         with np.load(path) as d:
             out = {k: d[k].copy() for k in d.files}
     with tempfile.TemporaryDirectory() as tmp:
@@ -65,7 +66,7 @@ def main():
             w, h, cf, gparams, _ = bench.CONFIGS[config]
             gops = bench.DEFAULT_GOPS[config]
             seed = 1729 + rank
-            if os.environ.get("MP2VG_DIGESTS_RESUME") and f"{config}_g{gops}_s{seed}" in out:
+            if resume and f"{config}_g{gops}_s{seed}" in out:
                 continue  # resuming an interrupted run: keep the finished cases
             es = R.generate_es(width=w, height=h, chroma_format=cf, n_gops=gops, seed=seed, **gparams)
             parsed = R.Parsed(es, w, h, cf, threads=8)

@@ -280,3 +280,42 @@ def test_reference_digests_for_every_rank_of_the_scaling_run(config, ranks):
     for r in range(ranks):
         exp = bench.expected_digests(config, bench.DEFAULT_GOPS[config], 1729 + r)
         assert exp is not None and len(exp) == 12 * bench.DEFAULT_GOPS[config], (config, r)
+
+
+def test_plain_bench_gpus_2_spawns_two_ranks():
+    """`python bench.py --gpus 2` (no launcher, the form of the driver's BENCH command) starts two
+    ranks itself -- one torch.distributed.run child, before any torch import or GPU call in the
+    parent -- and they form a world-2 group (gloo here; nccl on a GPU node)."""
+    import json
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2", "--backend", "gloo",
+                        "--probe-launch"], capture_output=True, text=True, timeout=240, cwd=repo, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1  # rank 0 only
+    assert lines[0]["n_gpus"] == 2 and lines[0]["ranks"] == [0, 1] and lines[0]["max_rank"] == 1.0
+
+
+def test_bench_refuses_a_world_that_does_not_match_gpus():
+    """Under a launcher, --gpus must equal the launched world (a --gpus 8 line can never come
+    from one rank)."""
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+               MASTER_PORT=str(_free_port_here()))
+    r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2", "--backend", "gloo",
+                        "--probe-launch"], capture_output=True, text=True, timeout=240, cwd=repo, env=env)
+    assert r.returncode != 0 and "--gpus 2 but the launcher started 1 rank" in r.stderr
+
+
+def _free_port_here():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p

@@ -164,11 +164,42 @@ def test_full_size_1080p_digest_vs_oracle():
         ctx.decode()
         ctx.synchronize()
         dig = ctx.digests(np.arange(parsed.npics))
-        for p in (0, parsed.npics - 1):
+        for p in range(parsed.npics):  # every frame byte for byte, not only its digest
             got = ctx.download(p)
-            assert all(np.array_equal(got[k], exp[p][k]) for k in range(3))
+            assert all(np.array_equal(got[k], exp[p][k]) for k in range(3)), p
     assert len(dig) == 12
     assert [int(x) for x in dig] == [R.planes_digest(f) for f in exp]
+
+
+def test_device_digest_catches_a_cancelling_lsb_pair():
+    """Two complementary LSB flips in one byte lane of two dwords of a decoded slot (the pair an
+    additive digest cancels, tests/test_digest.py) move the device digest, and the moved digest
+    is the host twin's digest of the flipped planes."""
+    import ctypes
+    from test_digest import additive_digest, cancelling_pair, flipped
+    from tiny_mp2v_dec_amd import _lib
+    from tiny_mp2v_dec_amd.decoder import _hip_lib
+    es = R.generate_es(width=176, height=144, chroma_format=1, n_gops=1, gop_n=12, gop_m=3, seed=31)
+    parsed = R.Parsed(es, 176, 144, 1)
+    with R.DeviceContext(176, 144, 1, slots=parsed.npics) as ctx:
+        ctx.upload(parsed.pics, parsed.mbs, parsed.coefs)
+        ctx.decode()
+        ctx.synchronize()
+        slot = parsed.npics - 1
+        planes = ctx.download(slot)
+        before = int(ctx.digests(np.array([slot]))[0])
+        assert before == R.planes_digest(planes)
+        x0, x1 = cancelling_pair(planes)
+        bad = flipped(planes, x0, x1)
+        assert additive_digest(bad) == additive_digest(planes)
+        ptr = ctypes.c_void_p()
+        _lib.check(_lib.lib().mp2vg_slot_device_ptr(ctx.h, slot, ctypes.byref(ptr)), "slot_device_ptr")
+        row = np.ascontiguousarray(bad[0][0])  # Y row 0 sits at the slot base (plane offset 0)
+        assert _hip_lib().hipMemcpy(ptr.value, row.ctypes.data, row.nbytes, 1) == 0  # host to device
+        after = int(ctx.digests(np.array([slot]))[0])
+        assert np.array_equal(ctx.download(slot)[0], bad[0])
+    assert after != before
+    assert after == R.planes_digest(bad)
 
 
 def test_back_to_back_batches_and_their_timing_events():

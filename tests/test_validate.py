@@ -124,3 +124,33 @@ def test_motion_vectors_outside_the_reference_rejected(cf):
         else:
             with pytest.raises(_lib.Mp2vgError, match="reads outside the reference"):
                 R.validate_batch(w, h, cf, p.npics, p.pics, mbs, p.coefs)
+
+
+@pytest.mark.parametrize("cf,seed", [(1, 11), (2, 12), (3, 13)])
+def test_parser_output_of_mutated_streams_passes_full_validation(cf, seed):
+    """The drop-in uploads its own parser's records on the trusted path (only picture-level
+    checks, usage and coefficient ranges: runtime.cpp uses_only), so the parser must uphold the
+    whole record contract on ANY input.  Byte-mutated and truncated streams that still parse must
+    produce batches that pass the full, untrusted validation (mp2vg_batch_validate)."""
+    w, h = 176, 144
+    es = R.generate_es(width=w, height=h, chroma_format=cf, n_gops=2, gop_n=6, gop_m=3,
+                       frame_pred_frame_dct=0 if cf != 3 else 1, seed=seed)
+    rng = np.random.default_rng(seed)
+    parsed_ok = 0
+    for trial in range(150):
+        b = bytearray(es)
+        if trial % 5 == 4:
+            b = b[:int(rng.integers(len(b) // 4, len(b)))]  # truncated
+        else:
+            for _ in range(int(rng.integers(1, 6))):
+                i = int(rng.integers(0, len(b)))
+                b[i] = int(rng.integers(0, 256)) if trial % 2 else b[i] ^ (1 << int(rng.integers(0, 8)))
+        try:
+            p = R.Parsed(bytes(b), w, h, cf)
+        except _lib.Mp2vgError:
+            continue
+        if p.npics == 0:
+            continue
+        parsed_ok += 1
+        R.validate_batch(w, h, cf, p.npics, p.pics, p.mbs, p.coefs)  # raises on any violation
+    assert parsed_ok > 10

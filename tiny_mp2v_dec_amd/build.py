@@ -94,28 +94,33 @@ def provenance():
     """What a log or bench line ran: the git commit (live in a checkout; on the GPU box, which gets
     the tree without .git, the commit build() recorded in _build/HEAD) and the library's content
     stamp (a SHA-256 over every source, header and build command: recomputable from any commit)."""
-    head = _git_head()
-    src = "git"
-    if head is None:
-        try:
-            with open(os.path.join(OUT, "HEAD")) as fh:
-                head, src = fh.read().strip() or None, "_build/HEAD (recorded by build())"
-        except OSError:
-            src = None
     try:
         with open(LIB + ".stamp") as fh:
             stamp = fh.read().strip()
     except OSError:
         stamp = None
-    return {"head": head, "head_source": src, "libmp2vg_stamp": stamp}
+    head = _git_head()
+    src = "git"
+    verified = None
+    if head is None:
+        # _build/HEAD: line 1 the commit, line 2 the library stamp build() produced at that commit.
+        # The head is vouched for only while the library loaded now is that same build
+        try:
+            with open(os.path.join(OUT, "HEAD")) as fh:
+                lines = fh.read().split()
+            head, src = (lines[0] if lines else None), "_build/HEAD (recorded by build())"
+            verified = len(lines) > 1 and stamp is not None and lines[1] == stamp
+        except OSError:
+            src = None
+    out = {"head": head, "head_source": src, "libmp2vg_stamp": stamp}
+    if verified is not None:
+        out["head_matches_library"] = verified
+    return out
 
 
 def build(verbose=False):
     os.makedirs(OUT, exist_ok=True)
     head = _git_head()
-    if head is not None:
-        with open(os.path.join(OUT, "HEAD"), "w") as fh:
-            fh.write(head + "\n")
     srcs = sorted(glob.glob(os.path.join(CSRC, "*.cpp")) + glob.glob(os.path.join(CSRC, "*.hip")))
     hdrs = _headers()
     objs = [os.path.join(OUT, os.path.basename(s) + ".o") for s in srcs]
@@ -138,6 +143,9 @@ def build(verbose=False):
         _write_stamp(LIB, lib_stamp)
         if verbose:
             print("linked", os.path.relpath(LIB, REPO))
+    if head is not None:  # the commit, and the library build() produced at it (provenance())
+        with open(os.path.join(OUT, "HEAD"), "w") as fh:
+            fh.write(f"{head}\n{lib_stamp}\n")
     # the reference CLI sample rebuilt against the drop-in header (include/mp2v_decoder.h)
     cli_src = os.path.join(REPO, "tools", "tiny_mp2v_dec_gpu.cpp")
     if os.path.exists(cli_src):

@@ -1190,8 +1190,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MCM == 0 &&
     }
 }
 // Order-independent 64-bit digest of a slot's visible planes:
-//   sum over visible dwords d at (row_id, byte x) of mix64((row_id << 32) | x) ^ d   (mod 2^64)
-// (rows numbered across Y, U, V).  tiny_mp2v_dec_amd.records.planes_digest is the host twin.
+//   sum over visible dwords d at (row_id, byte x) of mix64(mix64((row_id << 32) | x) ^ d)   (mod 2^64)
+// (rows numbered across Y, U, V).  The outer mix makes each term a pseudo-random function of the
+// dword, so sparse +-1 errors cannot cancel pairwise in the sum (an additive key ^ d term could).  tiny_mp2v_dec_amd.records.planes_digest is the host twin.
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
@@ -1220,7 +1221,7 @@ __global__ void digest_kernel(const uint8_t* __restrict__ pool, uint64_t slot_by
         }
         for (int x = threadIdx.x * 4; x < w; x += blockDim.x * 4) {
             const uint32_t d = *(const uint32_t*)(p + x);
-            acc += mix64(((uint64_t)row << 32) | (uint64_t)x) ^ (uint64_t)d;
+            acc += mix64(mix64(((uint64_t)row << 32) | (uint64_t)x) ^ (uint64_t)d);
         }
     }
     for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);

@@ -191,6 +191,8 @@ extern "C" int mp2vg_destroy(mp2vg_ctx_t* c) {
     if (c->ustream) hipStreamSynchronize(c->ustream);
     for (auto& h : c->hist) {
         for (auto e : h.l) hipEventDestroy(e);
+        for (auto e : h.s)
+            if (e) hipEventDestroy(e);
         for (auto e : h.b)
             if (e) hipEventDestroy(e);
     }
@@ -271,7 +273,11 @@ static int plan_batch(mp2vg_ctx_t* c, const mp2vg_picture_t* pics, int32_t npics
         if ((uint64_t)P.mb_first + nm > nmbs) return "picture MB range outside the batch";
         bool uses[2] = {false, false};
         for (uint64_t k = 0; k < nm; k++) {
-            const uint16_t f = mbs[P.mb_first + k].flags;
+            const mp2vg_mb_t& m = mbs[P.mb_first + k];
+            // the one O(MB) check kept on the trusted path: the kernel's coefficient loads of a
+            // P/B group are raw pointers, so a word range past the batch would read out of bounds
+            if ((uint64_t)m.coef_off + m.ncoef > ncoefs) return "MB coefficient range outside the batch";
+            const uint16_t f = m.flags;
             if (!(f & MP2VG_MB_INTRA)) {
                 uses[0] |= (f & MP2VG_MB_FWD) || !(f & MP2VG_MB_BWD);
                 uses[1] |= (f & MP2VG_MB_BWD) != 0;

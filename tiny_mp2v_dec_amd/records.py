@@ -223,7 +223,8 @@ def _mix64(z):
 
 def planes_digest(planes):
     """Host twin of the device digest (recon.hip digest_kernel): sum over visible dwords d at
-    (row_id, byte x), rows numbered across Y, U, V, of mix64((row_id << 32) | x) ^ d, mod 2^64."""
+    (row_id, byte x), rows numbered across Y, U, V, of mix64(mix64((row_id << 32) | x) ^ d), mod 2^64
+    (mixed after combining: paired small errors cannot cancel)."""
     total = np.uint64(0)
     row0 = 0
     with np.errstate(over="ignore"):
@@ -233,6 +234,6 @@ def planes_digest(planes):
             d = p.view("<u4").astype(np.uint64)  # (h, w/4)
             rows = (np.arange(h, dtype=np.uint64) + np.uint64(row0))[:, None]
             xs = (np.arange(w // 4, dtype=np.uint64) * np.uint64(4))[None, :]
-            total = total + np.sum(_mix64((rows << np.uint64(32)) | xs) ^ d, dtype=np.uint64)
+            total = total + np.sum(_mix64(_mix64((rows << np.uint64(32)) | xs) ^ d), dtype=np.uint64)
             row0 += h
     return int(total)
