@@ -20,6 +20,7 @@ run() {  # name, rocprof args...
 run ktrace --kernel-trace --stats || exit 1
 run fetch --kernel-trace --pmc FETCH_SIZE || exit 1
 run write --kernel-trace --pmc WRITE_SIZE || exit 1
+[ "${PASSES:-all}" = traffic ] && { run tcc --kernel-trace --pmc TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE || exit 1; echo done; exit 0; }
 run sq1 --kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES || exit 1
 run sq2 --kernel-trace --pmc SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_VMEM || exit 1
 run tcc --kernel-trace --pmc TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE || exit 1
