@@ -56,3 +56,27 @@ def test_mutated_streams_under_asan_ubsan(harness, names, seed):
     assert r.returncode == 0, (r.stdout[-500:], r.stderr[-3000:])
     res = json.loads(r.stdout.strip().splitlines()[-1])
     assert res["mutants_rejected"] > 0 and res["batches_rejected"] > 0 and res["batches_valid"] > 0
+
+
+@pytest.fixture(scope="module")
+def tsan_harness(tmp_path_factory):
+    """The same harness under ThreadSanitizer: every slice is a parse task, so the slices of one
+    picture run on several workers and publish the picture through an atomic countdown."""
+    exe = str(tmp_path_factory.mktemp("tsan") / "parse_fuzz")
+    cmd = ["g++", "-std=c++17", "-O1", "-g", "-w", "-fsanitize=thread", "-fno-omit-frame-pointer",
+           "-D__HIP_PLATFORM_AMD__", "-I", "/opt/rocm/include", "-I", CSRC, "-I", os.path.join(REPO, "include"),
+           os.path.join(REPO, "tests", "fuzz", "parse_fuzz.cpp"), os.path.join(CSRC, "parse.cpp"),
+           os.path.join(CSRC, "tables.cpp"), "-o", exe, "-pthread"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        pytest.skip(f"ThreadSanitizer build unavailable:\n{r.stderr[-800:]}")
+    return exe
+
+
+def test_slice_parallel_parse_under_tsan(tsan_harness):
+    env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1 exitcode=66")
+    r = subprocess.run([tsan_harness, "25", "4"] + _args(["hd1080_420_ipb", "ipb420_field", "ipb444_qcif",
+                                                          "stress_saturation"]),
+                       capture_output=True, text=True, timeout=900, env=env)
+    assert r.returncode == 0, (r.stdout[-500:], r.stderr[-3000:])
+    assert "WARNING: ThreadSanitizer" not in r.stderr

@@ -138,7 +138,7 @@ struct Ctx {
 
 // One slice -> its MB row of records (mb_decoder.cpp:521-641 for every MB of the slice).
 void parse_slice(const Ctx& C, const PicWork& P, const SliceJob& job, mp2vg_mb_t* row_base_all,
-                 std::vector<uint8_t>& row_done, SliceOut& out) {
+                 std::atomic<uint8_t>* row_done, SliceOut& out) {
     const Tables& T = Tables::get();
     const PictureHdr& h = P.hdr;
     const int pct = h.pct;
@@ -165,8 +165,8 @@ void parse_slice(const Ctx& C, const PicWork& P, const SliceJob& job, mp2vg_mb_t
     }
     br.skip(1);
     if (mb_row < 0 || mb_row >= C.mbh) FAIL(MP2VG_E_UNSUPPORTED, "slice row outside the picture");
-    if (row_done[mb_row]) FAIL(MP2VG_E_UNSUPPORTED, "two slices in one macroblock row");
-    row_done[mb_row] = 1;
+    // slices of one picture run on several workers: the row is claimed atomically
+    if (row_done[mb_row].exchange(1, std::memory_order_relaxed)) FAIL(MP2VG_E_UNSUPPORTED, "two slices in one macroblock row");
     out.mb_row = mb_row;
 
     // cache setup (decoder.cpp:125-145)
@@ -460,8 +460,10 @@ struct mp2vg_parsed : mp2vg::ParsedImpl {};
 using namespace mp2vg;
 
 // ---- parse session: pass 1 on the caller's thread, pass 2 on worker threads ---------------
-// Workers claim pictures in decode order; a picture's slices are parsed by one worker, which
-// then publishes the picture (status + its MB records).  mp2vg_parse_es waits for all of them;
+// Every slice is a task, as in the reference (decoder.cpp:316-318 queues one task per slice):
+// workers claim slices in decode order, so the slices of one picture run on several workers and
+// a picture is ready as soon as its last slice is; the worker that finishes it checks its row
+// coverage and publishes it (status + its MB records).  mp2vg_parse_es waits for all of them;
 // the drop-in decoder consumes pictures as they complete (decoder.cpp), overlapping the parse
 // with the device work.
 struct ParseSession {
@@ -469,13 +471,14 @@ struct ParseSession {
     mp2vg_parsed* res = nullptr;  // pictures, MB records (coef_off relative to the slice), display
     std::vector<SliceJob> jobs;
     std::vector<SliceOut> outs;
-    std::vector<std::vector<uint8_t>> row_done;
+    std::unique_ptr<std::atomic<uint8_t>[]> row_done;  // picture p's rows at [p * mbh, (p + 1) * mbh)
+    std::unique_ptr<std::atomic<int>[]> slices_left;   // per picture
     std::vector<size_t> pic_job_begin;
     std::vector<int> status;  // per picture: 1 pending, else an MP2VG_* status
     std::vector<std::string> err;
     std::mutex mu;
     std::condition_variable cv;
-    std::atomic<int> next_pic{0};
+    std::atomic<size_t> next_job{0};
     std::vector<std::thread> workers;
     size_t mbs_per_pic = 0;
     // Streaming (window > 0, the drop-in decoder): a worker parses picture p only once
@@ -505,49 +508,58 @@ struct ParseSession {
     }
     mp2vg_mb_t* mbs_of(int p) { return window ? pic_mbs[p] : res->mbs.data() + mbs_per_pic * p; }
     void work() {
-        const int npics = (int)C.pics.size();
         for (;;) {
-            const int p = next_pic.fetch_add(1);
-            if (p >= npics) return;
+            const size_t j = next_job.fetch_add(1);
+            if (j >= jobs.size()) return;
+            const int p = jobs[j].pic;
+            mp2vg_mb_t* mbs = nullptr;
             if (window) {
-                mp2vg_mb_t* b = nullptr;
-                {
-                    std::unique_lock<std::mutex> lk(mu);
-                    cv.wait(lk, [&] { return stop || p < consumed + window; });
-                    if (stop) return;
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return stop || p < consumed + window; });
+                if (stop) return;
+                if (!pic_mbs[p]) {  // the picture's first slice to get here gives it a buffer
                     if (!spare.empty()) {
-                        b = spare.back();
+                        pic_mbs[p] = spare.back();
                         spare.pop_back();
+                    } else {
+                        pic_mbs[p] = new mp2vg_mb_t[mbs_per_pic];  // every record is written by its slice
                     }
                 }
-                pic_mbs[p] = b ? b : new mp2vg_mb_t[mbs_per_pic];  // every record is written by its slice
+                mbs = pic_mbs[p];
+            } else {
+                mbs = mbs_of(p);
             }
-            int st = MP2VG_OK;
-            std::string msg;
-            for (size_t j = pic_job_begin[p]; j < pic_job_begin[p + 1]; j++) {
-                parse_slice(C, C.pics[p], jobs[j], mbs_of(p), row_done[p], outs[j]);
-                if (outs[j].status != MP2VG_OK && st == MP2VG_OK) {
-                    char m[256];
-                    snprintf(m, sizeof m, "picture %d slice @%llu: %s", p, (unsigned long long)jobs[j].byte_off,
-                             outs[j].err.c_str());
-                    st = outs[j].status;
-                    msg = m;
-                }
-            }
-            if (st == MP2VG_OK)
-                for (int r = 0; r < C.mbh; r++)
-                    if (!row_done[p][r]) {
-                        st = MP2VG_E_UNSUPPORTED;
-                        msg = "picture with a macroblock row not covered by any slice";
-                        break;
-                    }
-            {
-                std::lock_guard<std::mutex> lk(mu);
-                status[p] = st;
-                err[p] = msg;
-            }
-            cv.notify_all();
+            parse_slice(C, C.pics[p], jobs[j], mbs, &row_done[(size_t)p * C.mbh], outs[j]);
+            // the last slice of the picture publishes it (acq_rel: every slice's records and
+            // outputs are visible to the worker that finishes the picture)
+            if (slices_left[p].fetch_sub(1, std::memory_order_acq_rel) == 1) finish_picture(p);
         }
+    }
+    void finish_picture(int p) {
+        int st = MP2VG_OK;
+        std::string msg;
+        for (size_t j = pic_job_begin[p]; j < pic_job_begin[p + 1]; j++)  // first failing slice in stream order
+            if (outs[j].status != MP2VG_OK) {
+                char m[256];
+                snprintf(m, sizeof m, "picture %d slice @%llu: %s", p, (unsigned long long)jobs[j].byte_off,
+                         outs[j].err.c_str());
+                st = outs[j].status;
+                msg = m;
+                break;
+            }
+        if (st == MP2VG_OK)
+            for (int r = 0; r < C.mbh; r++)
+                if (!row_done[(size_t)p * C.mbh + r].load(std::memory_order_relaxed)) {
+                    st = MP2VG_E_UNSUPPORTED;
+                    msg = "picture with a macroblock row not covered by any slice";
+                    break;
+                }
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            status[p] = st;
+            err[p] = msg;
+        }
+        cv.notify_all();
     }
     int wait(int p) {
         std::unique_lock<std::mutex> lk(mu);
@@ -771,7 +783,10 @@ int parse_session_start(const uint8_t* buf, uint64_t len, const mp2vg_config_t* 
     for (auto& P : C.pics)
         for (auto& j : P.slices) S->jobs.push_back(j);
     S->outs.resize(S->jobs.size());
-    S->row_done.assign(npics, std::vector<uint8_t>(C.mbh, 0));
+    S->row_done.reset(new std::atomic<uint8_t>[(size_t)npics * C.mbh]);
+    for (size_t i = 0; i < (size_t)npics * C.mbh; i++) S->row_done[i].store(0, std::memory_order_relaxed);
+    S->slices_left.reset(new std::atomic<int>[npics]);
+    for (int p = 0; p < npics; p++) S->slices_left[p].store((int)C.pics[p].slices.size(), std::memory_order_relaxed);
     S->pic_job_begin.assign(npics + 1, 0);
     {
         size_t j = 0;
@@ -835,7 +850,7 @@ int parse_session_start(const uint8_t* buf, uint64_t len, const mp2vg_config_t* 
         if (held >= 0) res->display.push_back(held);
     }
     int nthreads = threads > 0 ? threads : (int)std::thread::hardware_concurrency();
-    nthreads = std::max(1, std::min(nthreads, std::max(1, npics)));
+    nthreads = std::max(1, std::min(nthreads, std::max(1, (int)S->jobs.size())));
     ParseSession* sp = S.get();
     for (int t = 0; t < nthreads; t++) sp->workers.emplace_back([sp]() { sp->work(); });
     *out = S.release();
