@@ -461,6 +461,8 @@ def main():
     if rank == 0 and world == 1 and dist is None and not args.no_e2e:
         result["e2e_dropin"] = e2e_dropin(es, width, height, cf, parsed.npics, device,
                                           result.get("cpu_baseline"))
+        result["e2e_dropin_device_frames"] = e2e_dropin(es, width, height, cf, parsed.npics, device,
+                                                        result.get("cpu_baseline"), device_frames=True)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if dist is not None:
@@ -469,11 +471,12 @@ def main():
         sys.exit(3)
 
 
-def e2e_dropin(es, width, height, cf, frames, device, cpu):
+def e2e_dropin(es, width, height, cf, frames, device, cpu, device_frames=False):
     """The drop-in API end to end on the same stream: mp2v_decoder_c(config, renderer).decode(buf)
     with host frame_c frames (parse, upload, decode, D2H, display-order render callbacks), i.e.
     what a caller of the reference API sees (reference tiny_mp2v_dec.cpp:50-55 times decode()
-    the same way).  PCIe-inclusive: never the bench `value`."""
+    the same way).  PCIe-inclusive: never the bench `value`.  device_frames: the opt-in
+    MP2VG_DECODER_DEVICE_FRAMES path (frames handed to the renderer in HBM, no D2H)."""
     from tiny_mp2v_dec_amd.decoder import decoder_config_t, mp2v_decoder_c
     share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 2)
     threads = max(2, min(share, os.cpu_count() or share, 16))
@@ -483,7 +486,7 @@ def e2e_dropin(es, width, height, cf, frames, device, cpu):
         count[0] += 1
 
     dec = mp2v_decoder_c(decoder_config_t(width, height, cf, pictures_pool_size=24, num_threads=threads,
-                                          device=device), render)
+                                          device=device, device_frames=device_frames), render)
     try:
         t = time.perf_counter()
         dec.decode(es, len(es))
@@ -494,7 +497,8 @@ def e2e_dropin(es, width, height, cf, frames, device, cpu):
         raise RuntimeError(f"drop-in rendered {count[0]} of {frames} frames")
     out = {"value": round(frames / dt, 1), "unit": "frames/s", "host_threads": threads, "frames": frames,
            "scope": "drop-in mp2v_decoder_c::decode() on the bench stream: host parse + record upload + "
-                    "GPU reconstruct + D2H into host frame_c + render callbacks"}
+                    + ("GPU reconstruct into device frame_c (HBM, no D2H) + render callbacks" if device_frames else
+                       "GPU reconstruct + D2H into host frame_c + render callbacks")}
     if cpu:
         out["vs_cpu_baseline"] = round(out["value"] / cpu["value"], 3)
     return out

@@ -491,7 +491,7 @@ __device__ __forceinline__ void issue_pass(const LaneRec& L, bool live, int lane
 }
 
 // ---- add/clip + store ----------------------------------------------------------------------
-template <int CF, int J, int NW, int ABL>
+template <int CF, int J, int NW, int ABL, bool ANCHOR = false>
 __device__ __forceinline__ void store_pass(uint32_t r0, uint32_t r1, bool live, int lane, const Geo& geo, uint8_t* wsink,
                                            uint8_t* dst_slot, const short* s_res_wave, const uint32_t (&p)[NW]) {
     using F = Fmt<CF>;
@@ -536,6 +536,27 @@ __device__ __forceinline__ void store_pass(uint32_t r0, uint32_t r1, bool live, 
     if (ABL & 8192)  // dev ablation (timing only): each store instruction writes 1 KB contiguous
         dst = dst_slot + ((((r0 & 0xffff) + (r0 >> 16) * 128u) * 3u + (uint32_t)J) * 1024u + (uint32_t)lane * 16u) %
                              (uint32_t)(geo.plane_off[1] - 1024);
+    if ((ABL & 16384) && ANCHOR && CF == 1) {
+        // dev ablation (timing only): the anchor pictures (I, P) also write the 128-B apron-tile
+        // copy the ABL 1024 taps read (the tile holding the row and, as its apron, the tile to its
+        // left): the store side of the tiled-anchor design, costed without building it
+        const uint32_t y = (r0 >> 16) * (plane == 0 ? 16u : 8u) + (uint32_t)py;
+        const uint32_t mx = r0 & 0xffff;
+        if (plane == 0) {
+            const uint32_t ncol = (uint32_t)geo.stride[0] >> 4;
+            const uint32_t t = mul24_asm(y >> 2, ncol) + mx;
+            const uint32_t o = (t * 128u + (y & 3u) * 32u) & 0x1FFFFFu;
+            const uint32_t oa = ((t - 1u) * 128u + (y & 3u) * 32u + 16u) & 0x1FFFFFu;
+            *(uint4*)(dst_slot + o) = make_uint4(out[0], out[1], out[2], out[3]);
+            *(uint4*)(dst_slot + oa) = make_uint4(out[0], out[1], out[2], out[3]);
+        } else {
+            const uint32_t ncol = (uint32_t)geo.stride[1] >> 3;
+            const uint32_t t = mul24_asm(y >> 3, ncol) + mx;
+            const uint32_t b = 0x200000u + (uint32_t)(plane - 1) * 0x70000u;
+            *(uint2*)(dst_slot + b + ((t * 128u + (y & 7u) * 16u) & 0x7FFFFu)) = make_uint2(out[0], out[1]);
+            *(uint2*)(dst_slot + b + (((t - 1u) * 128u + (y & 7u) * 16u + 8u) & 0x7FFFFu)) = make_uint2(out[0], out[1]);
+        }
+    }
     if (ABL & 8) {
         asm volatile("" ::"v"(out[0]), "v"(out[1]), "v"(out[2]), "v"(out[3]), "v"(dst));
     } else if (ABL & 4096) {  // dev ablation (timing only): one dword per row store (1/4, 1/2 bytes)
@@ -1109,9 +1130,9 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, LT&
             store_pass_put8<CF, 1, NWC>(gr0, glive, lane, geo, c.wsink, c.dst_slot, res8);
             if (CF != 1) store_pass_put8<CF, 2, NWC>(gr0, glive, lane, geo, c.wsink, c.dst_slot, res8);
         } else {
-            store_pass<CF, 0, 4, ABL>(gr0, gr1, glive, lane, geo, c.wsink, c.dst_slot, L.res[wave], p0);
-            store_pass<CF, 1, NWC, ABL>(gr0, gr1, glive, lane, geo, c.wsink, c.dst_slot, L.res[wave], p1);
-            if (CF != 1) store_pass<CF, 2, NWC, ABL>(gr0, gr1, glive, lane, geo, c.wsink, c.dst_slot, L.res[wave], p2);
+            store_pass<CF, 0, 4, ABL, MCM != 2>(gr0, gr1, glive, lane, geo, c.wsink, c.dst_slot, L.res[wave], p0);
+            store_pass<CF, 1, NWC, ABL, MCM != 2>(gr0, gr1, glive, lane, geo, c.wsink, c.dst_slot, L.res[wave], p1);
+            if (CF != 1) store_pass<CF, 2, NWC, ABL, MCM != 2>(gr0, gr1, glive, lane, geo, c.wsink, c.dst_slot, L.res[wave], p2);
         }
         wave_sync();
 
@@ -1259,7 +1280,8 @@ hipError_t launch_recon(int cf, int mcm, const KArgs& a, hipStream_t stream) {
     // -DMP2VG_DEV_ABLATIONS, tools/variant.sh EXTRA=...; 4:2:0, and 16 also 4:4:4): 1 no IDCT, 2 no
     // MC, 4 no dequant, 8 no stores, 16 stage stamps (tools/stamps.py), 32 MC loads out of range
     // (no address math), 64 no prediction arithmetic, 128 no 17th-pixel dwords, 512 no edge-row
-    // loads, 1024/2048/3072 tiled / all-hit taps, 4096/8192 store shapes.  Outputs are wrong under
+    // loads, 1024/2048/3072 tiled / all-hit taps, 4096/8192 store shapes, 16384 anchors also store
+    // the apron-tiled copy (17408 = with the tiled taps: the whole tiled-anchor design), 32768 none.  Outputs are wrong under
     // it (except 16); never set in tests or the bench.  A product library refuses the variable.
     static const int ablate = getenv("MP2VG_ABLATE") ? atoi(getenv("MP2VG_ABLATE")) : 0;
 #ifndef MP2VG_DEV_ABLATIONS
@@ -1286,6 +1308,9 @@ hipError_t launch_recon(int cf, int mcm, const KArgs& a, hipStream_t stream) {
         case 3072: return launch_mcm<1, 3072>(mcm, a, g, stream);
         case 4096: return launch_mcm<1, 4096>(mcm, a, g, stream);
         case 8192: return launch_mcm<1, 8192>(mcm, a, g, stream);
+        case 16384: return launch_mcm<1, 16384>(mcm, a, g, stream);
+        case 17408: return launch_mcm<1, 17408>(mcm, a, g, stream);  // 1024 | 16384: the tiled-anchor design
+        case 32768: return launch_mcm<1, 32768>(mcm, a, g, stream);  // no-op: the dev build's own baseline
         default: return hipErrorInvalidValue;
         }
     }

@@ -50,6 +50,14 @@ static int default_streams(const mp2vg_config_t* cfg) {
     const char* e = getenv("MP2VG_STREAMS");
     return e ? std::max(1, atoi(e)) : 2;
 }
+// how the picture sets' launch chains are coupled inside a batch (MP2VG_SET_COUPLE overrides for
+// measurements): 0 free-running streams; 1 lockstep (launch k of a set waits for launch k-1 of
+// every other set); 2 staggered (set s > 0 runs launch k after set s-1's launch k, and set s-1's
+// launch k+1 waits for set s's launch k-1: set s trails by one to two launches)
+static int set_coupling() {
+    const char* e = getenv("MP2VG_SET_COUPLE");
+    return e ? atoi(e) : 0;
+}
 
 // One resident record batch.  The context keeps two, so the upload of batch k+1 (on the copy
 // stream) overlaps the decode of batch k; an upload waits only for the decode that last read
@@ -78,6 +86,7 @@ struct mp2vg_ctx {
     hipStream_t ustream = nullptr;  // record uploads
     std::vector<hipStream_t> sstreams;  // one per picture set (created on first use)
     std::vector<hipEvent_t> sev;        // end of each set's launches in the last batch
+    std::vector<hipEvent_t> lev;        // end of each launch of the current batch (set coupling)
     std::vector<std::vector<uint8_t>> last_foot;  // slots each set of the last batch touched
     uint8_t* d_pool = nullptr;
     int32_t nslots = 0;
@@ -213,6 +222,7 @@ extern "C" int mp2vg_destroy(mp2vg_ctx_t* c) {
     if (c->h_stage) hipHostFree(c->h_stage);
     for (auto st : c->sstreams) hipStreamSynchronize(st);
     for (auto e : c->sev) hipEventDestroy(e);
+    for (auto e : c->lev) hipEventDestroy(e);
     for (auto st : c->sstreams) hipStreamDestroy(st);
     if (c->ustream) hipStreamDestroy(c->ustream);
     if (c->stream) hipStreamDestroy(c->stream);
@@ -635,14 +645,42 @@ extern "C" int mp2vg_batch_decode(mp2vg_ctx_t* c) {
     }
     for (int set = 0; set < nsets; set++) HIPCHK(hipEventRecord(H.s[set], stream_of(set)));
     H.ns = nsets;
-    for (int i = 0; i < nl; i++) {
-        const hipStream_t st = stream_of(launches[i].set);
-        a.slice_base = launches[i].begin;
-        a.nslices = launches[i].end - launches[i].begin;
-        if (c->launch_timing) HIPCHK(hipEventRecord(H.l[2 * i], st));
-        if (a.nslices) HIPCHK(launch_recon(c->g.cf, launches[i].mcm, a, st));
-        if (c->launch_timing) HIPCHK(hipEventRecord(H.l[2 * i + 1], st));
-    }
+    // launches are enqueued position by position across the sets (launch k of every set before
+    // launch k + 1 of any), so a coupling wait always names an event already recorded this batch
+    static const int couple = set_coupling();
+    std::vector<int> pos(nl), at;  // position of launch i in its set's chain; (set, position) -> i
+    std::vector<int> nper(nsets, 0);
+    for (int i = 0; i < nl; i++) pos[i] = nper[launches[i].set]++;
+    const int maxpos = *std::max_element(nper.begin(), nper.end());
+    at.assign((size_t)nsets * maxpos, -1);
+    for (int i = 0; i < nl; i++) at[(size_t)launches[i].set * maxpos + pos[i]] = i;
+    if (couple && nsets > 1)
+        while ((int)c->lev.size() < nl) {
+            hipEvent_t e;
+            HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            c->lev.push_back(e);
+        }
+    auto launch_at = [&](int set, int k) { return k >= 0 && k < nper[set] ? at[(size_t)set * maxpos + k] : -1; };
+    for (int k = 0; k < maxpos; k++)
+        for (int set = 0; set < nsets; set++) {
+            const int i = launch_at(set, k);
+            if (i < 0) continue;
+            const hipStream_t st = stream_of(set);
+            if (couple == 1 && nsets > 1) {
+                for (int t = 0; t < nsets; t++)
+                    if (t != set && launch_at(t, k - 1) >= 0) HIPCHK(hipStreamWaitEvent(st, c->lev[launch_at(t, k - 1)], 0));
+            } else if (couple == 2 && nsets > 1) {
+                if (set > 0 && launch_at(set - 1, k) >= 0) HIPCHK(hipStreamWaitEvent(st, c->lev[launch_at(set - 1, k)], 0));
+                if (set + 1 < nsets && launch_at(set + 1, k - 2) >= 0)
+                    HIPCHK(hipStreamWaitEvent(st, c->lev[launch_at(set + 1, k - 2)], 0));
+            }
+            a.slice_base = launches[i].begin;
+            a.nslices = launches[i].end - launches[i].begin;
+            if (c->launch_timing) HIPCHK(hipEventRecord(H.l[2 * i], st));
+            if (a.nslices) HIPCHK(launch_recon(c->g.cf, launches[i].mcm, a, st));
+            if (c->launch_timing) HIPCHK(hipEventRecord(H.l[2 * i + 1], st));
+            if (couple && nsets > 1) HIPCHK(hipEventRecord(c->lev[i], st));
+        }
     for (int set = 0; set < nsets; set++) {
         HIPCHK(hipEventRecord(c->sev[set], stream_of(set)));
         HIPCHK(hipStreamWaitEvent(c->stream, c->sev[set], 0));
