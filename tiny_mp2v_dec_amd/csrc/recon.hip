@@ -448,6 +448,103 @@ __device__ __forceinline__ void predict(Tap<NW>& tf, Tap<NW>& tb, int lane, uint
     for (int d = 0; d < NW; d++) p[d] = (uf && ub) ? avg4(pf[d], pb[d]) : (uf ? pf[d] : pb[d]);
 }
 
+// ---- 2-D luma taps (4:2:0 / 4:2:2 P and B pictures) ------------------------------------------
+// Lane (k, p, cx, m) = (lane & 3, (lane >> 2) & 1, (lane >> 3) & 1, lane >> 4) predicts pixels
+// 8cx..8cx+7 of two rows of MB k: frame MC rows 2p + 4m and 2p + 4m + 1, field MC rows p + 4m and
+// p + 4m + 2 (field p, its lines 2m and 2m + 1; p is also the lane's field-MC vector, as in
+// lane_rec).  Three reference rows per direction, each one dwordx3 from the dword-aligned x (the 9
+// pixels a half-pel row needs): the third row is the vertical half-pel partner of the second, so
+// there are no edge-row loads and no cross-lane second rows.  An instruction touches 32 reference
+// rows (two lanes per row, 20 contiguous bytes) instead of 64, and a direction is three
+// instructions instead of four.  The predicted rows go to the wave's prediction image in LDS,
+// from which the row-per-lane store pass reads them.
+#ifndef MP2VG_LUMA2D
+#define MP2VG_LUMA2D 0
+#endif
+template <int CF>
+struct Luma2D {
+    static constexpr bool on = MP2VG_LUMA2D && CF != 3;  // 4:4:4 P/B: the image would cost a workgroup per CU
+    static constexpr int PK = 68;                         // dwords per MB in the prediction image (64 + bank skew)
+};
+
+struct Tap2 {
+    uint32_t d[3][3];
+    uint32_t ctl;  // bits 0-1 byte shift, 2 half-pel x, 3 half-pel y, 4 used
+};
+
+template <int ABL>
+__device__ __forceinline__ void tap2_issue(Tap2& t, bool use, __amdgpu_buffer_rsrc_t ref, uint32_t mvw, uint32_t r0,
+                                           bool field, int fs, int stride, int lane) {
+    const int mvx = (short)(mvw & 0xffff), mvy = (short)(mvw >> 16);
+    const int p = (lane >> 2) & 1, cx = (lane >> 3) & 1, m = lane >> 4;
+    const int X = (int)(r0 & 0xffff) * 16 + cx * 8 + (mvx >> 1);
+    const int mby = (int)(r0 >> 16) * 16;
+    // frame MC (mb_decoder.cpp:212-228) rows y + (mvy >> 1); field MC (:229-236) rows
+    // field_select + 2 * (y / 2 + (mvy >> 1)) of the lane's field
+    const int Y = field ? mby + fs + 2 * (2 * m + (mvy >> 1)) : mby + 2 * p + 4 * m + (mvy >> 1);
+    t.ctl = (uint32_t)((X & 3) | ((mvx & 1) << 2) | ((mvy & 1) << 3) | ((int)use << 4));
+    const bool on = use && !(ABL & 32);
+    const uint32_t o = on ? (uint32_t)(X & ~3) + mul24_asm((uint32_t)Y, (uint32_t)stride) : kNoTap;
+    const uint32_t rs = on ? (uint32_t)(field ? 2 * stride : stride) : 0u;
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+        const u3v v = __builtin_amdgcn_raw_buffer_load_b96(ref, (int)(o + (uint32_t)i * rs), 0, 0);
+        t.d[i][0] = v.x; t.d[i][1] = v.y; t.d[i][2] = v.z;
+    }
+}
+
+// cascaded half-pel average (mc_sse2.hpp:5-39): each row averaged with its x+1 pixels (hx), then
+// output row j with row j+1 (hy); avg(r, r) == r makes both branch-free
+__device__ __forceinline__ void tap2_finish(const Tap2& t, uint32_t (&p)[4]) {
+    const uint32_t s = t.ctl & 3, hx = (t.ctl >> 2) & 1;
+    const bool hy = t.ctl & 8;
+    uint32_t r[3][2];
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+        const uint32_t a0 = __builtin_amdgcn_alignbyte(t.d[i][1], t.d[i][0], s);
+        const uint32_t a1 = __builtin_amdgcn_alignbyte(t.d[i][2], t.d[i][1], s);
+        const uint32_t a2 = t.d[i][2] >> (8 * s);  // byte 0: the 9th pixel
+        r[i][0] = avg4(a0, __builtin_amdgcn_alignbyte(a1, a0, hx));
+        r[i][1] = avg4(a1, __builtin_amdgcn_alignbyte(a2, a1, hx));
+    }
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+        p[2 * j] = avg4(r[j][0], hy ? r[j + 1][0] : r[j][0]);
+        p[2 * j + 1] = avg4(r[j][1], hy ? r[j + 1][1] : r[j][1]);
+    }
+}
+
+template <int MCM, int ABL>
+__device__ __forceinline__ void predict2(const Tap2& tf, const Tap2& tb, uint32_t (&p)[4]) {
+    if (ABL & 64) {
+#pragma unroll
+        for (int d = 0; d < 4; d++) p[d] = tf.d[d % 3][0] ^ tf.d[2][d % 3] ^ (MCM == 2 ? tb.d[d % 3][1] : 0u);
+        return;
+    }
+    const bool uf = tf.ctl & 16, ub = MCM == 2 && (tb.ctl & 16);
+    uint32_t pf[4] = {0, 0, 0, 0}, pb[4] = {0, 0, 0, 0};
+    if (uf) tap2_finish(tf, pf);
+    if (MCM == 2 && ub) tap2_finish(tb, pb);
+#pragma unroll
+    for (int d = 0; d < 4; d++) p[d] = (uf && ub) ? avg4(pf[d], pb[d]) : (uf ? pf[d] : pb[d]);
+}
+
+// the lane's two predicted half rows into the wave's prediction image: MB k at k * PK dwords,
+// row y at 4y, half cx at 2cx (the store pass reads row y of MB k as one 16-B LDS read)
+template <int PK>
+__device__ __forceinline__ void pimg_put(uint32_t* pw, int lane, bool field, const uint32_t (&p)[4]) {
+    const int k = lane & 3, pp = (lane >> 2) & 1, cx = (lane >> 3) & 1, m = lane >> 4;
+    const int row0 = field ? pp + 4 * m : 2 * pp + 4 * m;
+    uint32_t* a = pw + k * PK + row0 * 4 + cx * 2;
+    *(uint2*)a = make_uint2(p[0], p[1]);
+    *(uint2*)(a + (field ? 8 : 4)) = make_uint2(p[2], p[3]);
+}
+
+__device__ __forceinline__ void touch2(const Tap2& t) {
+#pragma unroll
+    for (int i = 0; i < 3; i++) asm volatile("" ::"v"(t.d[i][0]), "v"(t.d[i][1]), "v"(t.d[i][2]));
+}
+
 // per-lane record fields of the lane's MB that the tap issue needs
 struct LaneRec {
     uint32_t r0, r1, mvf, mvb;
@@ -488,6 +585,21 @@ __device__ __forceinline__ void issue_pass(const LaneRec& L, bool live, int lane
     if (MCM == 2)
         tap_issue<CF, NW, ABL>(tb, !none && bwd, ref_bwd, off, L.mvb, plane, gx, py, phm, mbyb, field,
                                (fl >> (9 + 2 * r)) & 1, stride, ph);
+}
+
+// the luma pass of issue_pass in the 2-D lane layout (Tap2)
+template <int MCM, int ABL = 0>
+__device__ __forceinline__ void issue_luma2(const LaneRec& L, bool live, int lane, const Geo& geo,
+                                            __amdgpu_buffer_rsrc_t ref_fwd, __amdgpu_buffer_rsrc_t ref_bwd, Tap2& tf,
+                                            Tap2& tb) {
+    const uint32_t fl = L.r1 & 0xffff;
+    const bool none = !live || (fl & MP2VG_MB_INTRA);
+    const bool bwd = fl & MP2VG_MB_BWD;
+    const bool fwd = !none && ((fl & MP2VG_MB_FWD) || !bwd);
+    const bool field = fl & MP2VG_MB_FIELD_MC;
+    const int r = field ? ((lane >> 2) & 1) : 0;
+    tap2_issue<ABL>(tf, fwd, ref_fwd, L.mvf, L.r0, field, (fl >> (8 + 2 * r)) & 1, geo.stride[0], lane);
+    if (MCM == 2) tap2_issue<ABL>(tb, !none && bwd, ref_bwd, L.mvb, L.r0, field, (fl >> (9 + 2 * r)) & 1, geo.stride[0], lane);
 }
 
 // ---- add/clip + store ----------------------------------------------------------------------
@@ -610,6 +722,9 @@ struct Lds {
     // residual images, int16 in ResLayout; C8 (intra only: output = clamp(residual)): the clamped
     // pixels as bytes in the same ResLayout order, half the size
     short res[WAVES][C8 ? G * ResLayout<CF>::SIZE / 2 : G * ResLayout<CF>::SIZE];
+    // P/B kernels with 2-D luma taps: the group's luma prediction (pimg_put), zero-length otherwise
+    static constexpr bool P2 = !C8 && Luma2D<CF>::on;
+    uint32_t pimg[P2 ? WAVES : 0][P2 ? G * Luma2D<CF>::PK : 0];
     uint8_t map[WAVES][MAXS];                    // slot -> k*16 + b
     uint32_t dq[WAVES][64];                      // (k*16 + b) -> dequant parameters (DqEntry)
     uint8_t W[4][64];
@@ -856,8 +971,12 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, LT&
     uint32_t g = c.mb_begin + wave * G;
     if (g >= mb_end) return;
     const int kl = lane & 3;
+    // 2-D luma taps (Tap2, prediction image in LDS) in the P/B loops of 4:2:0 / 4:2:2
+    constexpr bool L2D = LT::P2 && MCM != 0;
+    constexpr int PK = Luma2D<CF>::PK;
 
-    Tap<4> t0f, t0b;    // luma rows
+    Tap<4> t0f, t0b;    // luma rows (row-per-lane layout)
+    Tap2 u0f, u0b;      // luma rows (2-D layout)
     Tap<NWC> t1f, t1b;  // chroma rows (4:2:0: Cb + Cr; else Cb)
     Tap<NWC> t2f, t2b;  // Cr rows (4:2:2 / 4:4:4)
     Group S;
@@ -873,7 +992,10 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, LT&
         const int ng = (int)min(mb_end - g, (uint32_t)G);
         glive = kl < ng;
         const LaneRec R = lane_rec(rv, lane);
-        if (MCM) issue_pass<CF, MCM, 0, 4, ABL>(R, glive, lane, geo, c.ref_fwd, c.ref_bwd, t0f, t0b);
+        if constexpr (L2D)
+            issue_luma2<MCM, ABL>(R, glive, lane, geo, c.ref_fwd, c.ref_bwd, u0f, u0b);
+        else if (MCM)
+            issue_pass<CF, MCM, 0, 4, ABL>(R, glive, lane, geo, c.ref_fwd, c.ref_bwd, t0f, t0b);
         S = group_state<NB>(rv, ng);
         gr0 = R.r0;
         gr1 = R.r1;
@@ -906,11 +1028,23 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, LT&
 #pragma unroll
         for (int d = 0; d < NWC; d++) p1[d] = p2[d] = 0;
         if (MCM) {
-            touch(t0f), touch(t1f);
-            if (MCM == 2) touch(t0b), touch(t1b);
+            if constexpr (L2D) {
+                touch2(u0f);
+                if (MCM == 2) touch2(u0b);
+            } else {
+                touch(t0f);
+                if (MCM == 2) touch(t0b);
+            }
+            touch(t1f);
+            if (MCM == 2) touch(t1b);
             if (CF != 1) touch(t2f);
             if (CF != 1 && MCM == 2) touch(t2b);
-            predict<MCM, 4, ABL>(t0f, t0b, lane, p0);
+            if constexpr (L2D) {
+                predict2<MCM, ABL>(u0f, u0b, p0);
+                pimg_put<PK>(L.pimg[wave], lane, gr1 & MP2VG_MB_FIELD_MC, p0);
+            } else {
+                predict<MCM, 4, ABL>(t0f, t0b, lane, p0);
+            }
             predict<MCM, NWC, ABL>(t1f, t1b, lane, p1);
             if (CF != 1) predict<MCM, NWC, ABL>(t2f, t2b, lane, p2);
         }
@@ -921,7 +1055,10 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, LT&
         const int ngN = (int)min(mb_end - gn, (uint32_t)G);
         const bool gliveN = kl < ngN;
         const LaneRec R = lane_rec(rvN, lane);
-        if (MCM) issue_pass<CF, MCM, 0, 4, ABL>(R, gliveN, lane, geo, c.ref_fwd, c.ref_bwd, t0f, t0b);
+        if constexpr (L2D)
+            issue_luma2<MCM, ABL>(R, gliveN, lane, geo, c.ref_fwd, c.ref_bwd, u0f, u0b);
+        else if (MCM)
+            issue_pass<CF, MCM, 0, 4, ABL>(R, gliveN, lane, geo, c.ref_fwd, c.ref_bwd, t0f, t0b);
         const Group SN = group_state<NB>(rvN, ngN);
         __builtin_amdgcn_sched_barrier(0);
         rvN = rec_load(c.mbrec, g + 2 * STEP < mb_end ? g + 2 * STEP : g, mb_last, lane);
@@ -1130,6 +1267,10 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, LT&
             store_pass_put8<CF, 1, NWC>(gr0, glive, lane, geo, c.wsink, c.dst_slot, res8);
             if (CF != 1) store_pass_put8<CF, 2, NWC>(gr0, glive, lane, geo, c.wsink, c.dst_slot, res8);
         } else {
+            if constexpr (L2D) {  // row py = lane >> 2 of MB k = lane & 3 from the prediction image
+                const uint4 q = *(const uint4*)&L.pimg[wave][(lane & 3) * PK + (lane >> 2) * 4];
+                p0[0] = q.x, p0[1] = q.y, p0[2] = q.z, p0[3] = q.w;
+            }
             store_pass<CF, 0, 4, ABL, MCM != 2>(gr0, gr1, glive, lane, geo, c.wsink, c.dst_slot, L.res[wave], p0);
             store_pass<CF, 1, NWC, ABL, MCM != 2>(gr0, gr1, glive, lane, geo, c.wsink, c.dst_slot, L.res[wave], p1);
             if (CF != 1) store_pass<CF, 2, NWC, ABL, MCM != 2>(gr0, gr1, glive, lane, geo, c.wsink, c.dst_slot, L.res[wave], p2);

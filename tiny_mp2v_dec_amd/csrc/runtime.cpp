@@ -237,7 +237,14 @@ extern "C" int mp2vg_reserve_slots(mp2vg_ctx_t* c, int32_t nslots) {
     HIPCHK(hipStreamSynchronize(c->stream));
     uint8_t* p = nullptr;
     size_t bytes = (size_t)c->g.slot_bytes * nslots + kPoolPad;
-    HIPCHK(hipMalloc((void**)&p, bytes));
+    // dev knob for the pool-placement study (profiles/r4/README.md): 1 = physically contiguous
+    // (hipDeviceMallocContiguous, default allocation if the driver refuses it)
+    static const int pool_alloc = getenv("MP2VG_POOL_ALLOC") ? atoi(getenv("MP2VG_POOL_ALLOC")) : 0;
+    if (pool_alloc == 1 && hipExtMallocWithFlags((void**)&p, bytes, hipDeviceMallocContiguous) != hipSuccess) {
+        (void)hipGetLastError();
+        p = nullptr;
+    }
+    if (!p) HIPCHK(hipMalloc((void**)&p, bytes));
     HIPCHK(hipMemsetAsync(p, 0, bytes, c->stream));
     if (c->d_pool) {
         HIPCHK(hipMemcpyAsync(p, c->d_pool, (size_t)c->g.slot_bytes * c->nslots, hipMemcpyDeviceToDevice,
