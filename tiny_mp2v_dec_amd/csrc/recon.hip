@@ -449,15 +449,17 @@ __device__ __forceinline__ void predict(Tap<NW>& tf, Tap<NW>& tb, int lane, uint
 }
 
 // ---- 2-D luma taps (4:2:0 / 4:2:2 P and B pictures) ------------------------------------------
-// Lane (k, p, cx, m) = (lane & 3, (lane >> 2) & 1, (lane >> 3) & 1, lane >> 4) predicts pixels
-// 8cx..8cx+7 of two rows of MB k: frame MC rows 2p + 4m and 2p + 4m + 1, field MC rows p + 4m and
-// p + 4m + 2 (field p, its lines 2m and 2m + 1; p is also the lane's field-MC vector, as in
-// lane_rec).  Three reference rows per direction, each one dwordx3 from the dword-aligned x (the 9
-// pixels a half-pel row needs): the third row is the vertical half-pel partner of the second, so
-// there are no edge-row loads and no cross-lane second rows.  An instruction touches 32 reference
-// rows (two lanes per row, 20 contiguous bytes) instead of 64, and a direction is three
-// instructions instead of four.  The predicted rows go to the wave's prediction image in LDS,
-// from which the row-per-lane store pass reads them.
+// The luma taps in lane tiles of TW pixels x OR rows instead of one 16-px row per lane: lane
+// (k, p, cx, m) = (lane & 3, (lane >> 2) & 1, next log2(16 / TW) bits, the rest) predicts pixels
+// TW*cx .. TW*cx + TW-1 of OR rows of MB k: frame MC rows OR*(p + 2m) + j, field MC rows
+// p + 2*(OR*m + j) (field p, its lines OR*m + j; p is also the lane's field-MC vector, as in
+// lane_rec), j < OR.  OR + 1 reference rows per direction, each one load of TW/4 + 1 dwords from the
+// dword-aligned x (the TW + 1 pixels a half-pel row needs): the last row is the vertical half-pel
+// partner of the lane's last output row, so there are no edge-row loads and no cross-lane second
+// rows.  TW 8 (MP2VG_LUMA2D=1): three dwordx3 per direction, each touching 32 reference rows (two
+// lanes per row) instead of the row layout's four loads over 64; TW 4 (=2): five dwordx2 over 16
+// rows each.  The predicted rows go to the wave's prediction image in LDS, from which the
+// row-per-lane store pass reads them.
 #ifndef MP2VG_LUMA2D
 #define MP2VG_LUMA2D 0
 #endif
@@ -466,59 +468,77 @@ struct Luma2D {
     static constexpr bool on = MP2VG_LUMA2D && CF != 3;  // 4:4:4 P/B: the image would cost a workgroup per CU
     static constexpr int PK = 68;                         // dwords per MB in the prediction image (64 + bank skew)
 };
+constexpr int kTW = MP2VG_LUMA2D == 2 ? 4 : 8;  // tile width (pixels)
+constexpr int kOR = 64 / (4 * kTW);              // output rows per lane (2 or 4)
+constexpr int kNC = 16 / kTW;                    // tiles across an MB (2 or 4)
+constexpr int kND = kTW / 4 + 1;                 // dwords per reference row (3 or 2)
 
 struct Tap2 {
-    uint32_t d[3][3];
+    uint32_t d[kOR + 1][kND];
     uint32_t ctl;  // bits 0-1 byte shift, 2 half-pel x, 3 half-pel y, 4 used
 };
+__device__ __forceinline__ void tap2_lane(int lane, int& p, int& cx, int& m) {
+    p = (lane >> 2) & 1;
+    cx = (lane >> 3) & (kNC - 1);
+    m = lane >> (kNC == 2 ? 4 : 5);
+}
 
 template <int ABL>
 __device__ __forceinline__ void tap2_issue(Tap2& t, bool use, __amdgpu_buffer_rsrc_t ref, uint32_t mvw, uint32_t r0,
                                            bool field, int fs, int stride, int lane) {
     const int mvx = (short)(mvw & 0xffff), mvy = (short)(mvw >> 16);
-    const int p = (lane >> 2) & 1, cx = (lane >> 3) & 1, m = lane >> 4;
-    const int X = (int)(r0 & 0xffff) * 16 + cx * 8 + (mvx >> 1);
+    int p, cx, m;
+    tap2_lane(lane, p, cx, m);
+    const int X = (int)(r0 & 0xffff) * 16 + cx * kTW + (mvx >> 1);
     const int mby = (int)(r0 >> 16) * 16;
     // frame MC (mb_decoder.cpp:212-228) rows y + (mvy >> 1); field MC (:229-236) rows
     // field_select + 2 * (y / 2 + (mvy >> 1)) of the lane's field
-    const int Y = field ? mby + fs + 2 * (2 * m + (mvy >> 1)) : mby + 2 * p + 4 * m + (mvy >> 1);
+    const int Y = field ? mby + fs + 2 * (kOR * m + (mvy >> 1)) : mby + kOR * (p + 2 * m) + (mvy >> 1);
     t.ctl = (uint32_t)((X & 3) | ((mvx & 1) << 2) | ((mvy & 1) << 3) | ((int)use << 4));
     const bool on = use && !(ABL & 32);
     const uint32_t o = on ? (uint32_t)(X & ~3) + mul24_asm((uint32_t)Y, (uint32_t)stride) : kNoTap;
     const uint32_t rs = on ? (uint32_t)(field ? 2 * stride : stride) : 0u;
 #pragma unroll
-    for (int i = 0; i < 3; i++) {
-        const u3v v = __builtin_amdgcn_raw_buffer_load_b96(ref, (int)(o + (uint32_t)i * rs), 0, 0);
-        t.d[i][0] = v.x; t.d[i][1] = v.y; t.d[i][2] = v.z;
+    for (int i = 0; i <= kOR; i++) {
+        const int oi = (int)(o + (uint32_t)i * rs);
+        if constexpr (kND == 3) {
+            const u3v v = __builtin_amdgcn_raw_buffer_load_b96(ref, oi, 0, 0);
+            t.d[i][0] = v.x; t.d[i][1] = v.y; t.d[i][2] = v.z;
+        } else {
+            const uint2 v = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(ref, oi, 0, 0));
+            t.d[i][0] = v.x; t.d[i][1] = v.y;
+        }
     }
 }
 
 // cascaded half-pel average (mc_sse2.hpp:5-39): each row averaged with its x+1 pixels (hx), then
-// output row j with row j+1 (hy); avg(r, r) == r makes both branch-free
+// output row j with row j+1 (hy); avg(r, r) == r makes both branch-free.  p[j * (TW/4) + c] is
+// dword c of output row j.
 __device__ __forceinline__ void tap2_finish(const Tap2& t, uint32_t (&p)[4]) {
+    constexpr int NW = kTW / 4;
     const uint32_t s = t.ctl & 3, hx = (t.ctl >> 2) & 1;
     const bool hy = t.ctl & 8;
-    uint32_t r[3][2];
+    uint32_t r[kOR + 1][NW];
 #pragma unroll
-    for (int i = 0; i < 3; i++) {
-        const uint32_t a0 = __builtin_amdgcn_alignbyte(t.d[i][1], t.d[i][0], s);
-        const uint32_t a1 = __builtin_amdgcn_alignbyte(t.d[i][2], t.d[i][1], s);
-        const uint32_t a2 = t.d[i][2] >> (8 * s);  // byte 0: the 9th pixel
-        r[i][0] = avg4(a0, __builtin_amdgcn_alignbyte(a1, a0, hx));
-        r[i][1] = avg4(a1, __builtin_amdgcn_alignbyte(a2, a1, hx));
+    for (int i = 0; i <= kOR; i++) {
+        uint32_t a[NW + 1];
+#pragma unroll
+        for (int c = 0; c < NW; c++) a[c] = __builtin_amdgcn_alignbyte(t.d[i][c + 1], t.d[i][c], s);
+        a[NW] = t.d[i][NW] >> (8 * s);  // byte 0: the (TW+1)th pixel
+#pragma unroll
+        for (int c = 0; c < NW; c++) r[i][c] = avg4(a[c], __builtin_amdgcn_alignbyte(a[c + 1], a[c], hx));
     }
 #pragma unroll
-    for (int j = 0; j < 2; j++) {
-        p[2 * j] = avg4(r[j][0], hy ? r[j + 1][0] : r[j][0]);
-        p[2 * j + 1] = avg4(r[j][1], hy ? r[j + 1][1] : r[j][1]);
-    }
+    for (int j = 0; j < kOR; j++)
+#pragma unroll
+        for (int c = 0; c < NW; c++) p[j * NW + c] = avg4(r[j][c], hy ? r[j + 1][c] : r[j][c]);
 }
 
 template <int MCM, int ABL>
 __device__ __forceinline__ void predict2(const Tap2& tf, const Tap2& tb, uint32_t (&p)[4]) {
     if (ABL & 64) {
 #pragma unroll
-        for (int d = 0; d < 4; d++) p[d] = tf.d[d % 3][0] ^ tf.d[2][d % 3] ^ (MCM == 2 ? tb.d[d % 3][1] : 0u);
+        for (int d = 0; d < 4; d++) p[d] = tf.d[d % kOR][0] ^ tf.d[kOR][d % kND] ^ (MCM == 2 ? tb.d[d % kOR][1] : 0u);
         return;
     }
     const bool uf = tf.ctl & 16, ub = MCM == 2 && (tb.ctl & 16);
@@ -529,20 +549,29 @@ __device__ __forceinline__ void predict2(const Tap2& tf, const Tap2& tb, uint32_
     for (int d = 0; d < 4; d++) p[d] = (uf && ub) ? avg4(pf[d], pb[d]) : (uf ? pf[d] : pb[d]);
 }
 
-// the lane's two predicted half rows into the wave's prediction image: MB k at k * PK dwords,
-// row y at 4y, half cx at 2cx (the store pass reads row y of MB k as one 16-B LDS read)
+// the lane's predicted rows into the wave's prediction image: MB k at k * PK dwords, row y at 4y,
+// tile cx at cx * TW/4 (the store pass reads row y of MB k as one 16-B LDS read)
 template <int PK>
 __device__ __forceinline__ void pimg_put(uint32_t* pw, int lane, bool field, const uint32_t (&p)[4]) {
-    const int k = lane & 3, pp = (lane >> 2) & 1, cx = (lane >> 3) & 1, m = lane >> 4;
-    const int row0 = field ? pp + 4 * m : 2 * pp + 4 * m;
-    uint32_t* a = pw + k * PK + row0 * 4 + cx * 2;
-    *(uint2*)a = make_uint2(p[0], p[1]);
-    *(uint2*)(a + (field ? 8 : 4)) = make_uint2(p[2], p[3]);
+    int pp, cx, m;
+    tap2_lane(lane, pp, cx, m);
+    const int row0 = field ? pp + 2 * kOR * m : kOR * (pp + 2 * m);
+    uint32_t* a = pw + (lane & 3) * PK + row0 * 4 + cx * (kTW / 4);
+    const int rstep = field ? 8 : 4;
+#pragma unroll
+    for (int j = 0; j < kOR; j++) {
+        if constexpr (kTW == 8)
+            *(uint2*)(a + j * rstep) = make_uint2(p[2 * j], p[2 * j + 1]);
+        else
+            a[j * rstep] = p[j];
+    }
 }
 
 __device__ __forceinline__ void touch2(const Tap2& t) {
 #pragma unroll
-    for (int i = 0; i < 3; i++) asm volatile("" ::"v"(t.d[i][0]), "v"(t.d[i][1]), "v"(t.d[i][2]));
+    for (int i = 0; i <= kOR; i++)
+#pragma unroll
+        for (int c = 0; c < kND; c++) asm volatile("" ::"v"(t.d[i][c]));
 }
 
 // per-lane record fields of the lane's MB that the tap issue needs

@@ -49,7 +49,49 @@ def rows_of_pass(cf, plane_pass):
     return [(1, cw, ch), (2, cw, ch)]
 
 
-def picture_taps(P, mbs, stride, ph, plane_off, cf, layout):
+def luma2d_taps(P, mbs, stride, tw):
+    """Luma taps of the 2-D lane layout (recon.hip Tap2, MP2VG_LUMA2D): lane (k, p, cx, m) loads
+    OR + 1 rows of tw/4 + 1 dwords; instruction (direction, row i) spans every lane of the group.
+    Instruction ids: group * 64 + 40 + direction * 8 + i."""
+    n = len(mbs)
+    mbw = int(P["mb_width"])
+    x = mbs["x"].astype(np.int64)
+    y = mbs["y"].astype(np.int64)
+    fl = mbs["flags"].astype(np.int64)
+    grp = (np.arange(n) // mbw) * ((mbw + 3) // 4) + (x // 4)
+    inter = (fl & MB_INTRA) == 0
+    use = [inter & (((fl & MB_FWD) != 0) | ((fl & MB_BWD) == 0)), inter & ((fl & MB_BWD) != 0)]
+    field = (fl & MB_FIELD_MC) != 0
+    orr, nc, nd = 64 // (4 * tw), 16 // tw, tw // 4 + 1
+    st = stride[0]
+    ids_l, lines_l, sec_l = [], [], []
+    lanes = np.arange(16)  # per MB: (p, cx, m) of its 16 lanes
+    p = lanes & 1
+    cx = (lanes >> 1) & (nc - 1)
+    m = lanes >> (1 + (nc.bit_length() - 1))
+    for d in range(2):
+        u = use[d]
+        mvx = np.where(field[:, None], mbs["mv"][:, :, d, 0][:, p], mbs["mv"][:, 0, d, 0][:, None]).astype(np.int64)
+        mvy = np.where(field[:, None], mbs["mv"][:, :, d, 1][:, p], mbs["mv"][:, 0, d, 1][:, None]).astype(np.int64)
+        fs = (fl[:, None] >> (8 + 2 * p[None, :] + d)) & 1
+        X = x[:, None] * 16 + cx[None, :] * tw + (mvx >> 1)
+        Yf = y[:, None] * 16 + orr * (p[None, :] + 2 * m[None, :]) + (mvy >> 1)
+        Yd = y[:, None] * 16 + fs + 2 * (orr * m[None, :] + (mvy >> 1))
+        Y = np.where(field[:, None], Yd, Yf)
+        step = np.where(field[:, None], 2, 1)
+        sel = np.broadcast_to(u[:, None], Y.shape).ravel()
+        gid = np.broadcast_to(grp[:, None], Y.shape).ravel()
+        for i in range(orr + 1):
+            a = ((Y + i * step) * st + (X & ~3)).ravel()
+            ids = (gid * 64 + 40 + d * 8 + i)[sel]
+            for addr in (a[sel], a[sel] + 4 * nd - 1):
+                ids_l.append(ids)
+                lines_l.append(addr >> 7)
+                sec_l.append(addr >> 6)
+    return np.concatenate(ids_l), np.concatenate(lines_l), np.concatenate(sec_l), grp
+
+
+def picture_taps(P, mbs, stride, ph, plane_off, cf, layout, luma=True):
     """Arrays of (instruction id, line id, sector id) for every reference tap of one picture, and
     the group id of each instruction.  Instruction ids: group * 64 + kind."""
     n = len(mbs)
@@ -63,7 +105,7 @@ def picture_taps(P, mbs, stride, ph, plane_off, cf, layout):
     field = (fl & MB_FIELD_MC) != 0
     out_ids, out_lines, out_sec = [], [], []
     kind = 0
-    for ppass in (0, 1):
+    for ppass in ((0, 1) if luma else (1,)):
         for plane, pw, phm in rows_of_pass(cf, ppass):
             st = stride[plane]
             for d in range(2):
@@ -134,14 +176,19 @@ def main():
     plane_off = [0, stride[0] * ph[0], stride[0] * ph[0] + stride[1] * ph[1]]
     n = int(parsed.pics[0]["mb_width"]) * int(parsed.pics[0]["mb_height"])
     res = {}
-    for layout in ("linear", "apron", "tile8x16"):
+    for layout in ("linear", "apron", "tile8x16", "luma2d_tw8", "luma2d_tw4"):
         ta_l = ta_s = grp_l = groups = 0
         for p in range(parsed.npics):
             P = parsed.pics[p]
             if int(P["picture_coding_type"]) == 1:
                 continue
             mbs = parsed.mbs[int(P["mb_first"]):int(P["mb_first"]) + n]
-            ids, lines, secs, grp = picture_taps(P, mbs, stride, ph, plane_off, cf, layout)
+            if layout.startswith("luma2d"):
+                ids, lines, secs, grp = picture_taps(P, mbs, stride, ph, plane_off, cf, "linear", luma=False)
+                i2, l2, s2, _ = luma2d_taps(P, mbs, stride, int(layout[-1]))
+                ids, lines, secs = np.concatenate([ids, i2]), np.concatenate([lines, l2]), np.concatenate([secs, s2])
+            else:
+                ids, lines, secs, grp = picture_taps(P, mbs, stride, ph, plane_off, cf, layout)
             ta_l += count_unique(ids, lines)
             ta_s += count_unique(ids, secs)
             grp_l += count_unique(ids // 64, lines)
