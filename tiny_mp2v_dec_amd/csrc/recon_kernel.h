@@ -43,7 +43,8 @@ struct Launch {
 // per-launch geometry, passed by value
 struct Geo {
     uint8_t* sink;  // 16+ writable, readable bytes outside every slot: dummy loads and stores
-    uint64_t slot_bytes;
+    uint64_t slot_bytes;   // one picture (frame_c layout): the reference rows' buffer size
+    uint64_t slot_stride;  // slot i starts at pool + i * slot_stride (>= slot_bytes)
     uint32_t plane_off[3];  // plane offsets inside a slot (a slot is < 4 GiB)
     int32_t stride[3];
     int32_t ph[3];
@@ -56,7 +57,7 @@ struct KArgs {
     const SliceDesc* slices;
     uint8_t* pool;
     uint8_t* sink;
-    uint64_t slot_bytes;
+    uint64_t slot_bytes, slot_stride;
     uint64_t plane_off[3];
     int32_t stride[3];
     int32_t ph[3];

@@ -20,7 +20,7 @@
 
 namespace mp2vg {
 hipError_t launch_recon(int cf, int mcm, const KArgs& a, hipStream_t stream);
-hipError_t launch_digest(const uint8_t* pool, uint64_t slot_bytes, const int32_t* d_slots, int n,
+hipError_t launch_digest(const uint8_t* pool, uint64_t slot_stride, const int32_t* d_slots, int n,
                          const uint64_t off[3], const int32_t stride[3], const int32_t w[3],
                          const int32_t h[3], unsigned long long* d_out, hipStream_t stream);
 }  // namespace mp2vg
@@ -54,6 +54,13 @@ static int default_streams(const mp2vg_config_t* cfg) {
 // measurements): 0 free-running streams; 1 lockstep (launch k of a set waits for launch k-1 of
 // every other set); 2 staggered (set s > 0 runs launch k after set s-1's launch k, and set s-1's
 // launch k+1 waits for set s's launch k-1: set s trails by one to two launches)
+// Bytes between consecutive frame slots beyond the slot itself (MP2VG_SLOT_PAD overrides for the
+// pool-placement measurements, profiles/r4/README.md): slot offsets decide which HBM channels the
+// same pixel rows of different pictures land on.
+static size_t slot_pad() {
+    const char* e = getenv("MP2VG_SLOT_PAD");
+    return e ? (size_t)std::max(0, atoi(e)) & ~(size_t)255 : 0;
+}
 static int set_coupling() {
     const char* e = getenv("MP2VG_SET_COUPLE");
     return e ? atoi(e) : 0;
@@ -90,6 +97,7 @@ struct mp2vg_ctx {
     std::vector<std::vector<uint8_t>> last_foot;  // slots each set of the last batch touched
     uint8_t* d_pool = nullptr;
     int32_t nslots = 0;
+    size_t slot_stride = 0;  // bytes from one slot to the next: the slot size plus slot_pad()
     int nstreams = 2;  // independent picture sets per batch (default_streams)
 
     Bank bank[2];
@@ -170,6 +178,7 @@ extern "C" int mp2vg_create(const mp2vg_config_t* cfg, mp2vg_ctx_t** out) {
     mp2vg_ctx_t* c = new mp2vg_ctx_t();
     c->cfg = *cfg;
     c->g.init(cfg->width, cfg->height, cfg->chroma_format);
+    c->slot_stride = c->g.slot_bytes + slot_pad();
     c->nstreams = default_streams(cfg);
     bool ok = true;
     for (Bank& b : c->bank)
@@ -236,7 +245,7 @@ extern "C" int mp2vg_reserve_slots(mp2vg_ctx_t* c, int32_t nslots) {
     if (nslots <= c->nslots) return MP2VG_OK;
     HIPCHK(hipStreamSynchronize(c->stream));
     uint8_t* p = nullptr;
-    size_t bytes = (size_t)c->g.slot_bytes * nslots + kPoolPad;
+    size_t bytes = c->slot_stride * nslots + kPoolPad;
     // dev knob for the pool-placement study (profiles/r4/README.md): 1 = physically contiguous
     // (hipDeviceMallocContiguous, default allocation if the driver refuses it)
     static const int pool_alloc = getenv("MP2VG_POOL_ALLOC") ? atoi(getenv("MP2VG_POOL_ALLOC")) : 0;
@@ -247,7 +256,7 @@ extern "C" int mp2vg_reserve_slots(mp2vg_ctx_t* c, int32_t nslots) {
     if (!p) HIPCHK(hipMalloc((void**)&p, bytes));
     HIPCHK(hipMemsetAsync(p, 0, bytes, c->stream));
     if (c->d_pool) {
-        HIPCHK(hipMemcpyAsync(p, c->d_pool, (size_t)c->g.slot_bytes * c->nslots, hipMemcpyDeviceToDevice,
+        HIPCHK(hipMemcpyAsync(p, c->d_pool, c->slot_stride * c->nslots, hipMemcpyDeviceToDevice,
                               c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
         HIPCHK(hipFree(c->d_pool));
@@ -610,8 +619,9 @@ extern "C" int mp2vg_batch_decode(mp2vg_ctx_t* c) {
     a.coefs = b.d_coefs;
     a.slices = b.d_slices;
     a.pool = c->d_pool;
-    a.sink = c->d_pool + (size_t)c->g.slot_bytes * c->nslots + kSinkOff;
+    a.sink = c->d_pool + c->slot_stride * c->nslots + kSinkOff;
     a.slot_bytes = c->g.slot_bytes;
+    a.slot_stride = c->slot_stride;
     for (int i = 0; i < 3; i++) {
         a.plane_off[i] = c->g.plane_off[i];
         a.stride[i] = c->g.stride[i];
@@ -778,7 +788,7 @@ extern "C" int mp2vg_download_slot(mp2vg_ctx_t* c, int32_t slot, uint8_t* dst[3]
     HIPCHK(hipStreamSynchronize(c->stream));
     for (int p = 0; p < 3; p++) {
         size_t ds = (dst_stride && dst_stride[p]) ? (size_t)dst_stride[p] : (size_t)c->g.pw[p];
-        const uint8_t* src = c->d_pool + (size_t)slot * c->g.slot_bytes + c->g.plane_off[p];
+        const uint8_t* src = c->d_pool + (size_t)slot * c->slot_stride + c->g.plane_off[p];
         HIPCHK(hipMemcpy2DAsync(dst[p], ds, src, c->g.stride[p], c->g.pw[p], c->g.ph[p], hipMemcpyDeviceToHost,
                                 c->stream));
     }
@@ -793,7 +803,7 @@ extern "C" int mp2vg_copy_slot_packed(mp2vg_ctx_t* c, int32_t slot, void* dst, i
     uint8_t* d = (uint8_t*)dst;
     const hipMemcpyKind kind = dst_on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
     for (int p = 0; p < 3; p++) {
-        const uint8_t* src = c->d_pool + (size_t)slot * c->g.slot_bytes + c->g.plane_off[p];
+        const uint8_t* src = c->d_pool + (size_t)slot * c->slot_stride + c->g.plane_off[p];
         HIPCHK(hipMemcpy2DAsync(d, c->g.pw[p], src, c->g.stride[p], c->g.pw[p], c->g.ph[p], kind, c->stream));
         d += (size_t)c->g.pw[p] * c->g.ph[p];
     }
@@ -803,7 +813,7 @@ extern "C" int mp2vg_copy_slot_packed(mp2vg_ctx_t* c, int32_t slot, void* dst, i
 
 extern "C" int mp2vg_slot_device_ptr(mp2vg_ctx_t* c, int32_t slot, void** dptr) {
     if (!c || !dptr || slot < 0 || slot >= c->nslots) return MP2VG_E_INVALID;
-    *dptr = c->d_pool + (size_t)slot * c->g.slot_bytes;
+    *dptr = c->d_pool + (size_t)slot * c->slot_stride;
     return MP2VG_OK;
 }
 
@@ -826,7 +836,7 @@ extern "C" int mp2vg_slot_digests(mp2vg_ctx_t* c, const int32_t* slots, int32_t 
     int32_t st[3] = {c->g.stride[0], c->g.stride[1], c->g.stride[2]};
     int32_t w[3] = {c->g.pw[0], c->g.pw[1], c->g.pw[2]};
     int32_t h[3] = {c->g.ph[0], c->g.ph[1], c->g.ph[2]};
-    HIPCHK(launch_digest(c->d_pool, c->g.slot_bytes, c->d_dslots, n, c->g.plane_off, st, w, h, c->d_digest, c->stream));
+    HIPCHK(launch_digest(c->d_pool, c->slot_stride, c->d_dslots, n, c->g.plane_off, st, w, h, c->d_digest, c->stream));
     HIPCHK(hipMemcpyAsync(out, c->d_digest, sizeof(uint64_t) * n, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     return MP2VG_OK;
