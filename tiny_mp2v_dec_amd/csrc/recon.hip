@@ -298,6 +298,28 @@ __device__ __forceinline__ void pass_row(int lane, int& k, int& plane, int& py) 
     }
 }
 
+// ---- anchor tiles ---------------------------------------------------------------------------
+// The taps read reference pictures (I and P: the anchors) from a second, tiled copy that the
+// anchor's own store pass writes next to its frame_c rows (the tile slot of frame slot i, plane p
+// at 2 * plane_off[p]).  A W-px plane (luma and 4:4:4 chroma: W = 16; 4:2:0 / 4:2:2 chroma: W = 8)
+// is cut into 128-B tiles, one cache line each: 4 rows x 32 B (W 16) or 8 rows x 16 B (W 8), tile
+// t of a band holding pixels [W t, W t + 2 W) -- its own W pixels and, as an apron, the next
+// tile's.  A tap row (W + 1 pixels from the dword-aligned x) therefore lies in one tile row, and
+// the 17 rows of a luma tap touch 5-6 lines instead of 17 (profiles/r4/README.md: B launch -21 %).
+// Tile (band b, column t) sits at (b * ncol + t) * 128 with ncol = stride / W.
+template <int W>  // byte offset, in its tile plane, of pixel (x & ~3, y): the tap's row start
+__device__ __forceinline__ uint32_t tile_off(uint32_t x, uint32_t y, uint32_t ncol) {
+    if (W == 16) return (mul24_asm(y >> 2, ncol) + (x >> 4)) * 128u + (y & 3u) * 32u + (x & 12u);
+    return (mul24_asm(y >> 3, ncol) + (x >> 3)) * 128u + (y & 7u) * 16u + (x & 4u);
+}
+// the two places of the W-px row segment of MB column mx at row y: its own tile (returned) and,
+// at own - 128 + W, the apron of the tile to its left
+template <int W>
+__device__ __forceinline__ uint32_t tile_row(uint32_t mx, uint32_t y, uint32_t ncol) {
+    if (W == 16) return (mul24_asm(y >> 2, ncol) + mx) * 128u + (y & 3u) * 32u;
+    return (mul24_asm(y >> 3, ncol) + mx) * 128u + (y & 7u) * 16u;
+}
+
 // ---- motion compensation taps ---------------------------------------------------------------
 // One prediction direction of one pixel row: NW+1 raw dwords of reference row Y from the
 // dword-aligned x, loaded one group ahead.  The second row of a vertical half-pel average
@@ -337,7 +359,12 @@ __device__ __forceinline__ void load_row(uint32_t (&d)[NW + 1], __amdgpu_buffer_
     }
 }
 
-template <int CF, int NW, int ABL = 0>
+#ifndef MP2VG_CHROMA_TILES
+#define MP2VG_CHROMA_TILES 1
+#endif
+constexpr bool kChromaTiles = MP2VG_CHROMA_TILES;  // dev A/B: 0 = chroma taps from the frame rows
+
+template <int CF, int NW, int ABL = 0, bool TL = true>
 __device__ __forceinline__ void tap_issue(Tap<NW>& t, bool use, __amdgpu_buffer_rsrc_t ref, uint32_t plane_off,
                                           uint32_t mvw, int plane, int gx, int py, int phm, int mby_base, bool field,
                                           int fs, int stride, int ph) {
@@ -364,24 +391,16 @@ __device__ __forceinline__ void tap_issue(Tap<NW>& t, bool use, __amdgpu_buffer_
     const int hx = mvx & 1, hy = mvy & 1;
     const bool edge = py + step >= phm;
     t.ctl = (uint32_t)((Xc & 3) | (hx << 2) | (hy << 3) | ((int)use << 4) | ((int)edge << 5) | ((int)field << 6));
-    // dword-aligned row start: byte-exact (unaligned) buffer loads would save two alignbytes per
-    // dword but cost twice the texture-address cycles, a net loss (tools/unaligned_check.hip)
-    const uint32_t row = plane_off + (uint32_t)(Xc & ~3);
-    uint32_t o0 = (use && !(ABL & 32)) ? row + mul24_asm((uint32_t)Y0, (uint32_t)stride) : kNoTap;
-    uint32_t o1 = (use && hy && edge && !(ABL & 32)) ? row + mul24_asm((uint32_t)Y1, (uint32_t)stride) : kNoTap;
-    if (ABL & 1024) {  // dev ablation (timing only): apron-tiled addresses, 128-B tiles of 4 x 32 B
-        const uint32_t A = (uint32_t)(Xc & ~3);  // luma (4 rows x 32 B) / chroma (8 rows x 16 B)
-        const uint32_t ncol = (uint32_t)stride >> (plane == 0 ? 4 : 3);
-        auto toff = [&](int yy) -> uint32_t {
-            const uint32_t y = (uint32_t)yy;
-            if (plane == 0)
-                return ((mul24_asm(y >> 2, ncol) + (A >> 4)) * 128u + (y & 3u) * 32u + (A & 12u)) & 0x1FFFFFu;
-            return 0x200000u + (uint32_t)(plane - 1) * 0x70000u +
-                   (((mul24_asm(y >> 3, ncol) + (A >> 3)) * 128u + (y & 7u) * 16u + (A & 4u)) & 0x7FFFFu);
-        };
-        o0 = use ? toff(Y0) : kNoTap;
-        o1 = (use && hy && edge) ? toff(Y1) : kNoTap;
-    }
+    // the rows come from the reference's anchor tiles (tile_off), from the dword-aligned x:
+    // byte-exact (unaligned) buffer loads would save two alignbytes per dword but cost twice the
+    // texture-address cycles, a net loss (tools/unaligned_check.hip)
+    const uint32_t ncol = (uint32_t)stride >> (NW == 4 ? 4 : 3);
+    auto toff = [&](int y) -> uint32_t {
+        return TL ? plane_off + tile_off<4 * NW>((uint32_t)Xc, (uint32_t)y, ncol)
+                  : plane_off + (uint32_t)(Xc & ~3) + mul24_asm((uint32_t)y, (uint32_t)stride);
+    };
+    uint32_t o0 = (use && !(ABL & 32)) ? toff(Y0) : kNoTap;
+    uint32_t o1 = (use && hy && edge && !(ABL & 32)) ? toff(Y1) : kNoTap;
     if (ABL & 2048) {  // dev ablation (timing only): every tap inside a 64-KB window (L1/L2 hits)
         o0 = o0 == kNoTap ? kNoTap : (o0 & 0xFFFFu);
         o1 = o1 == kNoTap ? kNoTap : (o1 & 0xFFFFu);
@@ -448,132 +467,6 @@ __device__ __forceinline__ void predict(Tap<NW>& tf, Tap<NW>& tb, int lane, uint
     for (int d = 0; d < NW; d++) p[d] = (uf && ub) ? avg4(pf[d], pb[d]) : (uf ? pf[d] : pb[d]);
 }
 
-// ---- 2-D luma taps (4:2:0 / 4:2:2 P and B pictures) ------------------------------------------
-// The luma taps in lane tiles of TW pixels x OR rows instead of one 16-px row per lane: lane
-// (k, p, cx, m) = (lane & 3, (lane >> 2) & 1, next log2(16 / TW) bits, the rest) predicts pixels
-// TW*cx .. TW*cx + TW-1 of OR rows of MB k: frame MC rows OR*(p + 2m) + j, field MC rows
-// p + 2*(OR*m + j) (field p, its lines OR*m + j; p is also the lane's field-MC vector, as in
-// lane_rec), j < OR.  OR + 1 reference rows per direction, each one load of TW/4 + 1 dwords from the
-// dword-aligned x (the TW + 1 pixels a half-pel row needs): the last row is the vertical half-pel
-// partner of the lane's last output row, so there are no edge-row loads and no cross-lane second
-// rows.  TW 8 (MP2VG_LUMA2D=1): three dwordx3 per direction, each touching 32 reference rows (two
-// lanes per row) instead of the row layout's four loads over 64; TW 4 (=2): five dwordx2 over 16
-// rows each.  The predicted rows go to the wave's prediction image in LDS, from which the
-// row-per-lane store pass reads them.
-#ifndef MP2VG_LUMA2D
-#define MP2VG_LUMA2D 0
-#endif
-template <int CF>
-struct Luma2D {
-    static constexpr bool on = MP2VG_LUMA2D && CF != 3;  // 4:4:4 P/B: the image would cost a workgroup per CU
-    static constexpr int PK = 68;                         // dwords per MB in the prediction image (64 + bank skew)
-};
-constexpr int kTW = MP2VG_LUMA2D == 2 ? 4 : 8;  // tile width (pixels)
-constexpr int kOR = 64 / (4 * kTW);              // output rows per lane (2 or 4)
-constexpr int kNC = 16 / kTW;                    // tiles across an MB (2 or 4)
-constexpr int kND = kTW / 4 + 1;                 // dwords per reference row (3 or 2)
-
-struct Tap2 {
-    uint32_t d[kOR + 1][kND];
-    uint32_t ctl;  // bits 0-1 byte shift, 2 half-pel x, 3 half-pel y, 4 used
-};
-__device__ __forceinline__ void tap2_lane(int lane, int& p, int& cx, int& m) {
-    p = (lane >> 2) & 1;
-    cx = (lane >> 3) & (kNC - 1);
-    m = lane >> (kNC == 2 ? 4 : 5);
-}
-
-template <int ABL>
-__device__ __forceinline__ void tap2_issue(Tap2& t, bool use, __amdgpu_buffer_rsrc_t ref, uint32_t mvw, uint32_t r0,
-                                           bool field, int fs, int stride, int lane) {
-    const int mvx = (short)(mvw & 0xffff), mvy = (short)(mvw >> 16);
-    int p, cx, m;
-    tap2_lane(lane, p, cx, m);
-    const int X = (int)(r0 & 0xffff) * 16 + cx * kTW + (mvx >> 1);
-    const int mby = (int)(r0 >> 16) * 16;
-    // frame MC (mb_decoder.cpp:212-228) rows y + (mvy >> 1); field MC (:229-236) rows
-    // field_select + 2 * (y / 2 + (mvy >> 1)) of the lane's field
-    const int Y = field ? mby + fs + 2 * (kOR * m + (mvy >> 1)) : mby + kOR * (p + 2 * m) + (mvy >> 1);
-    t.ctl = (uint32_t)((X & 3) | ((mvx & 1) << 2) | ((mvy & 1) << 3) | ((int)use << 4));
-    const bool on = use && !(ABL & 32);
-    const uint32_t o = on ? (uint32_t)(X & ~3) + mul24_asm((uint32_t)Y, (uint32_t)stride) : kNoTap;
-    const uint32_t rs = on ? (uint32_t)(field ? 2 * stride : stride) : 0u;
-#pragma unroll
-    for (int i = 0; i <= kOR; i++) {
-        const int oi = (int)(o + (uint32_t)i * rs);
-        if constexpr (kND == 3) {
-            const u3v v = __builtin_amdgcn_raw_buffer_load_b96(ref, oi, 0, 0);
-            t.d[i][0] = v.x; t.d[i][1] = v.y; t.d[i][2] = v.z;
-        } else {
-            const uint2 v = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(ref, oi, 0, 0));
-            t.d[i][0] = v.x; t.d[i][1] = v.y;
-        }
-    }
-}
-
-// cascaded half-pel average (mc_sse2.hpp:5-39): each row averaged with its x+1 pixels (hx), then
-// output row j with row j+1 (hy); avg(r, r) == r makes both branch-free.  p[j * (TW/4) + c] is
-// dword c of output row j.
-__device__ __forceinline__ void tap2_finish(const Tap2& t, uint32_t (&p)[4]) {
-    constexpr int NW = kTW / 4;
-    const uint32_t s = t.ctl & 3, hx = (t.ctl >> 2) & 1;
-    const bool hy = t.ctl & 8;
-    uint32_t r[kOR + 1][NW];
-#pragma unroll
-    for (int i = 0; i <= kOR; i++) {
-        uint32_t a[NW + 1];
-#pragma unroll
-        for (int c = 0; c < NW; c++) a[c] = __builtin_amdgcn_alignbyte(t.d[i][c + 1], t.d[i][c], s);
-        a[NW] = t.d[i][NW] >> (8 * s);  // byte 0: the (TW+1)th pixel
-#pragma unroll
-        for (int c = 0; c < NW; c++) r[i][c] = avg4(a[c], __builtin_amdgcn_alignbyte(a[c + 1], a[c], hx));
-    }
-#pragma unroll
-    for (int j = 0; j < kOR; j++)
-#pragma unroll
-        for (int c = 0; c < NW; c++) p[j * NW + c] = avg4(r[j][c], hy ? r[j + 1][c] : r[j][c]);
-}
-
-template <int MCM, int ABL>
-__device__ __forceinline__ void predict2(const Tap2& tf, const Tap2& tb, uint32_t (&p)[4]) {
-    if (ABL & 64) {
-#pragma unroll
-        for (int d = 0; d < 4; d++) p[d] = tf.d[d % kOR][0] ^ tf.d[kOR][d % kND] ^ (MCM == 2 ? tb.d[d % kOR][1] : 0u);
-        return;
-    }
-    const bool uf = tf.ctl & 16, ub = MCM == 2 && (tb.ctl & 16);
-    uint32_t pf[4] = {0, 0, 0, 0}, pb[4] = {0, 0, 0, 0};
-    if (uf) tap2_finish(tf, pf);
-    if (MCM == 2 && ub) tap2_finish(tb, pb);
-#pragma unroll
-    for (int d = 0; d < 4; d++) p[d] = (uf && ub) ? avg4(pf[d], pb[d]) : (uf ? pf[d] : pb[d]);
-}
-
-// the lane's predicted rows into the wave's prediction image: MB k at k * PK dwords, row y at 4y,
-// tile cx at cx * TW/4 (the store pass reads row y of MB k as one 16-B LDS read)
-template <int PK>
-__device__ __forceinline__ void pimg_put(uint32_t* pw, int lane, bool field, const uint32_t (&p)[4]) {
-    int pp, cx, m;
-    tap2_lane(lane, pp, cx, m);
-    const int row0 = field ? pp + 2 * kOR * m : kOR * (pp + 2 * m);
-    uint32_t* a = pw + (lane & 3) * PK + row0 * 4 + cx * (kTW / 4);
-    const int rstep = field ? 8 : 4;
-#pragma unroll
-    for (int j = 0; j < kOR; j++) {
-        if constexpr (kTW == 8)
-            *(uint2*)(a + j * rstep) = make_uint2(p[2 * j], p[2 * j + 1]);
-        else
-            a[j * rstep] = p[j];
-    }
-}
-
-__device__ __forceinline__ void touch2(const Tap2& t) {
-#pragma unroll
-    for (int i = 0; i <= kOR; i++)
-#pragma unroll
-        for (int c = 0; c < kND; c++) asm volatile("" ::"v"(t.d[i][c]));
-}
-
 // per-lane record fields of the lane's MB that the tap issue needs
 struct LaneRec {
     uint32_t r0, r1, mvf, mvb;
@@ -608,33 +501,40 @@ __device__ __forceinline__ void issue_pass(const LaneRec& L, bool live, int lane
     const int r = field ? (py & 1) : 0;
     const int stride = gsel(geo.stride, plane);
     const int ph = gsel(geo.ph, plane);
-    const uint32_t off = (uint32_t)gsel(geo.plane_off, plane);
-    tap_issue<CF, NW, ABL>(tf, fwd, ref_fwd, off, L.mvf, plane, gx, py, phm, mbyb, field, (fl >> (8 + 2 * r)) & 1,
-                           stride, ph);
+    constexpr bool TL = J == 0 || kChromaTiles;
+    const uint32_t off = (TL ? 2u : 1u) * (uint32_t)gsel(geo.plane_off, plane);  // the plane in the tile slot
+    tap_issue<CF, NW, ABL, TL>(tf, fwd, ref_fwd, off, L.mvf, plane, gx, py, phm, mbyb, field, (fl >> (8 + 2 * r)) & 1,
+                               stride, ph);
     if (MCM == 2)
-        tap_issue<CF, NW, ABL>(tb, !none && bwd, ref_bwd, off, L.mvb, plane, gx, py, phm, mbyb, field,
-                               (fl >> (9 + 2 * r)) & 1, stride, ph);
-}
-
-// the luma pass of issue_pass in the 2-D lane layout (Tap2)
-template <int MCM, int ABL = 0>
-__device__ __forceinline__ void issue_luma2(const LaneRec& L, bool live, int lane, const Geo& geo,
-                                            __amdgpu_buffer_rsrc_t ref_fwd, __amdgpu_buffer_rsrc_t ref_bwd, Tap2& tf,
-                                            Tap2& tb) {
-    const uint32_t fl = L.r1 & 0xffff;
-    const bool none = !live || (fl & MP2VG_MB_INTRA);
-    const bool bwd = fl & MP2VG_MB_BWD;
-    const bool fwd = !none && ((fl & MP2VG_MB_FWD) || !bwd);
-    const bool field = fl & MP2VG_MB_FIELD_MC;
-    const int r = field ? ((lane >> 2) & 1) : 0;
-    tap2_issue<ABL>(tf, fwd, ref_fwd, L.mvf, L.r0, field, (fl >> (8 + 2 * r)) & 1, geo.stride[0], lane);
-    if (MCM == 2) tap2_issue<ABL>(tb, !none && bwd, ref_bwd, L.mvb, L.r0, field, (fl >> (9 + 2 * r)) & 1, geo.stride[0], lane);
+        tap_issue<CF, NW, ABL, TL>(tb, !none && bwd, ref_bwd, off, L.mvb, plane, gx, py, phm, mbyb, field,
+                                   (fl >> (9 + 2 * r)) & 1, stride, ph);
 }
 
 // ---- add/clip + store ----------------------------------------------------------------------
-template <int CF, int J, int NW, int ABL, bool ANCHOR = false>
+// An anchor row's two tile copies (tile_off): its own tile and the apron of the tile to its left
+// (MB column 0 has none).  Dead lanes write the wave's sink line.
+template <int NW>
+__device__ __forceinline__ void tile_store(uint8_t* tplane, uint32_t mx, uint32_t y, uint32_t ncol, bool live,
+                                           uint8_t* wsink, const uint32_t (&out)[4]) {
+    constexpr int W = 4 * NW;
+    const uint32_t o = tile_row<W>(mx, y, ncol);
+    uint8_t* d0 = live ? tplane + o : wsink;
+    uint8_t* d1 = (live && mx) ? tplane + (o - 128u + W) : wsink;
+    if (NW == 4) {
+        *(uint4*)d0 = make_uint4(out[0], out[1], out[2], out[3]);
+        *(uint4*)d1 = make_uint4(out[0], out[1], out[2], out[3]);
+    } else {
+        *(uint2*)d0 = make_uint2(out[0], out[1]);
+        *(uint2*)d1 = make_uint2(out[0], out[1]);
+    }
+}
+
+// tiles (uniform: the picture is read by a later one, runtime.cpp TilePlan): the row also goes
+// to the picture's anchor tiles (tile_store)
+template <int CF, int J, int NW, int ABL>
 __device__ __forceinline__ void store_pass(uint32_t r0, uint32_t r1, bool live, int lane, const Geo& geo, uint8_t* wsink,
-                                           uint8_t* dst_slot, const short* s_res_wave, const uint32_t (&p)[NW]) {
+                                           uint8_t* dst_slot, uint8_t* dst_tiles, bool tiles, const short* s_res_wave,
+                                           const uint32_t (&p)[NW]) {
     using F = Fmt<CF>;
     using RL = ResLayout<CF>;
     int k, plane, py;
@@ -677,26 +577,12 @@ __device__ __forceinline__ void store_pass(uint32_t r0, uint32_t r1, bool live, 
     if (ABL & 8192)  // dev ablation (timing only): each store instruction writes 1 KB contiguous
         dst = dst_slot + ((((r0 & 0xffff) + (r0 >> 16) * 128u) * 3u + (uint32_t)J) * 1024u + (uint32_t)lane * 16u) %
                              (uint32_t)(geo.plane_off[1] - 1024);
-    if ((ABL & 16384) && ANCHOR && CF == 1) {
-        // dev ablation (timing only): the anchor pictures (I, P) also write the 128-B apron-tile
-        // copy the ABL 1024 taps read (the tile holding the row and, as its apron, the tile to its
-        // left): the store side of the tiled-anchor design, costed without building it
-        const uint32_t y = (r0 >> 16) * (plane == 0 ? 16u : 8u) + (uint32_t)py;
-        const uint32_t mx = r0 & 0xffff;
-        if (plane == 0) {
-            const uint32_t ncol = (uint32_t)geo.stride[0] >> 4;
-            const uint32_t t = mul24_asm(y >> 2, ncol) + mx;
-            const uint32_t o = (t * 128u + (y & 3u) * 32u) & 0x1FFFFFu;
-            const uint32_t oa = ((t - 1u) * 128u + (y & 3u) * 32u + 16u) & 0x1FFFFFu;
-            *(uint4*)(dst_slot + o) = make_uint4(out[0], out[1], out[2], out[3]);
-            *(uint4*)(dst_slot + oa) = make_uint4(out[0], out[1], out[2], out[3]);
-        } else {
-            const uint32_t ncol = (uint32_t)geo.stride[1] >> 3;
-            const uint32_t t = mul24_asm(y >> 3, ncol) + mx;
-            const uint32_t b = 0x200000u + (uint32_t)(plane - 1) * 0x70000u;
-            *(uint2*)(dst_slot + b + ((t * 128u + (y & 7u) * 16u) & 0x7FFFFu)) = make_uint2(out[0], out[1]);
-            *(uint2*)(dst_slot + b + (((t - 1u) * 128u + (y & 7u) * 16u + 8u) & 0x7FFFFu)) = make_uint2(out[0], out[1]);
-        }
+    if (tiles) {  // the row's pixels for tile_group: over the first half of its (read) int16 residual row
+        uint8_t* img = (uint8_t*)(s_res_wave + k * RL::SIZE + RL::base(plane) + py * RL::width(plane));
+        if (NW == 4)
+            *(uint4*)img = make_uint4(out[0], out[1], out[2], out[3]);
+        else
+            *(uint2*)img = make_uint2(out[0], out[1]);
     }
     if (ABL & 8) {
         asm volatile("" ::"v"(out[0]), "v"(out[1]), "v"(out[2]), "v"(out[3]), "v"(dst));
@@ -735,6 +621,84 @@ __device__ __forceinline__ void store_pass_put8(uint32_t r0, bool live, int lane
     }
 }
 
+// I kernels: the group's anchor tiles written from the byte residual image in whole tile lines.
+// A group of 4 MBs (columns t0..t0+3) owns tiles t0..t0+2 of each band completely and two half
+// tiles: t0+3's own half (MB 3) and t0-1's apron half (MB 0; none at column 0).  Unit u of a
+// W-16 plane: u < 96 -> tile t0 + (u >> 5), band (u >> 3) & 3 of the MB row, chunk u & 7 (row
+// chunk >> 1, half chunk & 1: MB j + half), so 8 consecutive lanes fill one 128-B line; 96..127 ->
+// the half tiles' 16-B rows.  A W-8 plane (4:2:0 / 4:2:2 chroma): 16-B units are whole tile rows
+// [MB j row | MB j+1 row] of tiles t0..t0+2, 8-B units the half tiles' rows.  Row stores of the
+// same bytes (tile_store, one row per lane) left 16-B pieces 32 B apart in every line.
+// a row of the group's pixels from LDS: the I kernels' byte residual image (compact layout, each
+// dword in the x0, x0+2, x0+1, x0+3 order of ResLayout: one v_perm); P/B kernels (NAT): the
+// final pixels in natural order that store_pass left in the first half of each int16 residual row
+template <int CF, bool NAT>
+__device__ __forceinline__ const uint8_t* img_row(const uint8_t* img, int k, int plane, int py) {
+    using RL = ResLayout<CF>;
+    return &img[(NAT ? 2 : 1) * (k * RL::SIZE + RL::base(plane) + py * RL::width(plane))];
+}
+__device__ __forceinline__ uint32_t unswz(uint32_t v, bool nat) { return nat ? v : __builtin_amdgcn_perm(v, v, 0x03010200u); }
+template <int CF, bool NAT>
+__device__ __forceinline__ uint4 img_row16(const uint8_t* img, int k, int plane, int py) {
+    const uint4 q = *(const uint4*)img_row<CF, NAT>(img, k, plane, py);
+    return make_uint4(unswz(q.x, NAT), unswz(q.y, NAT), unswz(q.z, NAT), unswz(q.w, NAT));
+}
+template <int CF, bool NAT>
+__device__ __forceinline__ uint2 img_row8(const uint8_t* img, int k, int plane, int py) {
+    const uint2 q = *(const uint2*)img_row<CF, NAT>(img, k, plane, py);
+    return make_uint2(unswz(q.x, NAT), unswz(q.y, NAT));
+}
+template <int CF, bool NAT>
+__device__ __forceinline__ void tile_group(uint32_t mx0, uint32_t mby, int lane, const Geo& geo, uint8_t* wsink,
+                                           uint8_t* dst_tiles, const uint8_t* res8) {
+    using F = Fmt<CF>;
+    // W-16 planes: luma, and the 4:4:4 chroma planes
+    for (int plane = 0; plane < (CF == 3 && kChromaTiles ? 3 : 1); plane++) {
+        uint8_t* tp = dst_tiles + 2u * gsel(geo.plane_off, plane);
+        const uint32_t ncol = (uint32_t)gsel(geo.stride, plane) >> 4;
+#pragma nounroll
+        for (int i = 0; i < 2; i++) {
+            const int u = lane + 64 * i;
+            int j, r, h;
+            if (u < 96) {
+                j = u >> 5, r = ((u >> 3) & 3) * 4 + ((u & 7) >> 1), h = u & 1;
+            } else {
+                const int side = (u - 96) >> 4;
+                r = u & 15, h = side, j = side ? -1 : 3;
+            }
+            const uint4 v = img_row16<CF, NAT>(res8, j + h, plane, r);
+            const bool none = j < 0 && mx0 == 0;
+            const uint32_t o = tile_row<16>(mx0 + (uint32_t)j, mby * 16u + (uint32_t)r, ncol) + (uint32_t)h * 16u;
+            *(uint4*)(none ? wsink : tp + o) = v;
+        }
+    }
+    if constexpr (CF != 3 && kChromaTiles) {  // W-8 chroma: Cb and Cr
+        constexpr int RPM = F::CH;  // chroma rows per MB (8 or 16)
+        constexpr int N16 = 2 * 3 * RPM, N8 = 2 * 2 * RPM;
+        const uint32_t ncol = (uint32_t)geo.stride[1] >> 3;
+#pragma nounroll
+        for (int i = 0; i < (N16 + 63) / 64; i++) {
+            const int u = lane + 64 * i;
+            const int plane = 1 + (u >= 3 * RPM ? 1 : 0), rem = u - (plane - 1) * 3 * RPM;
+            const int j = rem / RPM, r = rem % RPM;
+            const uint2 a = img_row8<CF, NAT>(res8, j, plane, r), b = img_row8<CF, NAT>(res8, min(j + 1, 3), plane, r);
+            const uint32_t o = tile_row<8>(mx0 + (uint32_t)j, mby * (uint32_t)RPM + (uint32_t)r, ncol);
+            *(uint4*)(u < N16 ? dst_tiles + 2u * gsel(geo.plane_off, plane) + o : wsink) = make_uint4(a.x, a.y, b.x, b.y);
+        }
+#pragma nounroll
+        for (int i = 0; i < (N8 + 63) / 64; i++) {
+            const int u = lane + 64 * i;
+            const int plane = 1 + (u >= 2 * RPM ? 1 : 0), rem = u - (plane - 1) * 2 * RPM;
+            const int side = rem / RPM, r = rem % RPM;
+            const int j = side ? -1 : 3, h = side;
+            const uint2 v = img_row8<CF, NAT>(res8, side ? 0 : 3, plane, r);
+            const uint32_t o = tile_row<8>(mx0 + (uint32_t)j, mby * (uint32_t)RPM + (uint32_t)r, ncol) + (uint32_t)h * 8u;
+            const bool none = u >= N8 || (side && mx0 == 0);
+            *(uint2*)(none ? wsink : dst_tiles + 2u * gsel(geo.plane_off, plane) + o) = v;
+        }
+    }
+}
+
 // ---- one slice ------------------------------------------------------------------------------
 constexpr int BLKS = 72;
 // C8 = the compact layout of the I kernels (4:4:4: 38.4 KB instead of 53.8 KB per workgroup, so
@@ -751,9 +715,6 @@ struct Lds {
     // residual images, int16 in ResLayout; C8 (intra only: output = clamp(residual)): the clamped
     // pixels as bytes in the same ResLayout order, half the size
     short res[WAVES][C8 ? G * ResLayout<CF>::SIZE / 2 : G * ResLayout<CF>::SIZE];
-    // P/B kernels with 2-D luma taps: the group's luma prediction (pimg_put), zero-length otherwise
-    static constexpr bool P2 = !C8 && Luma2D<CF>::on;
-    uint32_t pimg[P2 ? WAVES : 0][P2 ? G * Luma2D<CF>::PK : 0];
     uint8_t map[WAVES][MAXS];                    // slot -> k*16 + b
     uint32_t dq[WAVES][64];                      // (k*16 + b) -> dequant parameters (DqEntry)
     uint8_t W[4][64];
@@ -836,10 +797,13 @@ struct SliceCtx {
     const uint32_t* mbrec;
     const uint32_t* coefs;
     uint8_t* dst_slot;
+    uint8_t* dst_tiles;  // the picture's anchor tiles
+    bool tiles;          // ... which it writes (SliceDesc.reserved bit 0, runtime.cpp TilePlan)
     // this wave's own 64-B sink line (dummy and dead-lane stores): stores of many waves to one
     // address serialize in one L2 channel, and a wave's first loop-head wait covers its own
     uint8_t* wsink;
     __amdgpu_buffer_rsrc_t ref_fwd, ref_bwd;
+    __amdgpu_buffer_rsrc_t cref_fwd, cref_bwd;  // chroma taps' source (the tiles, or frame rows)
     __amdgpu_buffer_rsrc_t coef_rsrc;  // the batch's words; offsets >= kNoTap read nothing
     uint32_t mb_begin, mb_end;
 };
@@ -1000,12 +964,8 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, LT&
     uint32_t g = c.mb_begin + wave * G;
     if (g >= mb_end) return;
     const int kl = lane & 3;
-    // 2-D luma taps (Tap2, prediction image in LDS) in the P/B loops of 4:2:0 / 4:2:2
-    constexpr bool L2D = LT::P2 && MCM != 0;
-    constexpr int PK = Luma2D<CF>::PK;
 
-    Tap<4> t0f, t0b;    // luma rows (row-per-lane layout)
-    Tap2 u0f, u0b;      // luma rows (2-D layout)
+    Tap<4> t0f, t0b;    // luma rows
     Tap<NWC> t1f, t1b;  // chroma rows (4:2:0: Cb + Cr; else Cb)
     Tap<NWC> t2f, t2b;  // Cr rows (4:2:2 / 4:4:4)
     Group S;
@@ -1021,10 +981,7 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, LT&
         const int ng = (int)min(mb_end - g, (uint32_t)G);
         glive = kl < ng;
         const LaneRec R = lane_rec(rv, lane);
-        if constexpr (L2D)
-            issue_luma2<MCM, ABL>(R, glive, lane, geo, c.ref_fwd, c.ref_bwd, u0f, u0b);
-        else if (MCM)
-            issue_pass<CF, MCM, 0, 4, ABL>(R, glive, lane, geo, c.ref_fwd, c.ref_bwd, t0f, t0b);
+        if (MCM) issue_pass<CF, MCM, 0, 4, ABL>(R, glive, lane, geo, c.ref_fwd, c.ref_bwd, t0f, t0b);
         S = group_state<NB>(rv, ng);
         gr0 = R.r0;
         gr1 = R.r1;
@@ -1033,8 +990,8 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, LT&
         prefetch_words<MCM, NCW>(cw, c, S.coef0, S.ncoef, lane);
         __builtin_amdgcn_sched_barrier(0);
         if (MCM) {
-            issue_pass<CF, MCM, 1, NWC, ABL>(R, glive, lane, geo, c.ref_fwd, c.ref_bwd, t1f, t1b);
-            if (CF != 1) issue_pass<CF, MCM, 2, NWC, ABL>(R, glive, lane, geo, c.ref_fwd, c.ref_bwd, t2f, t2b);
+            issue_pass<CF, MCM, 1, NWC, ABL>(R, glive, lane, geo, c.cref_fwd, c.cref_bwd, t1f, t1b);
+            if (CF != 1) issue_pass<CF, MCM, 2, NWC, ABL>(R, glive, lane, geo, c.cref_fwd, c.cref_bwd, t2f, t2b);
         }
         __builtin_amdgcn_sched_barrier(0);
         // the steady-state loop issues the group's stores after these loads: dummy stores to the
@@ -1057,23 +1014,11 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, LT&
 #pragma unroll
         for (int d = 0; d < NWC; d++) p1[d] = p2[d] = 0;
         if (MCM) {
-            if constexpr (L2D) {
-                touch2(u0f);
-                if (MCM == 2) touch2(u0b);
-            } else {
-                touch(t0f);
-                if (MCM == 2) touch(t0b);
-            }
-            touch(t1f);
-            if (MCM == 2) touch(t1b);
+            touch(t0f), touch(t1f);
+            if (MCM == 2) touch(t0b), touch(t1b);
             if (CF != 1) touch(t2f);
             if (CF != 1 && MCM == 2) touch(t2b);
-            if constexpr (L2D) {
-                predict2<MCM, ABL>(u0f, u0b, p0);
-                pimg_put<PK>(L.pimg[wave], lane, gr1 & MP2VG_MB_FIELD_MC, p0);
-            } else {
-                predict<MCM, 4, ABL>(t0f, t0b, lane, p0);
-            }
+            predict<MCM, 4, ABL>(t0f, t0b, lane, p0);
             predict<MCM, NWC, ABL>(t1f, t1b, lane, p1);
             if (CF != 1) predict<MCM, NWC, ABL>(t2f, t2b, lane, p2);
         }
@@ -1084,10 +1029,7 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, LT&
         const int ngN = (int)min(mb_end - gn, (uint32_t)G);
         const bool gliveN = kl < ngN;
         const LaneRec R = lane_rec(rvN, lane);
-        if constexpr (L2D)
-            issue_luma2<MCM, ABL>(R, gliveN, lane, geo, c.ref_fwd, c.ref_bwd, u0f, u0b);
-        else if (MCM)
-            issue_pass<CF, MCM, 0, 4, ABL>(R, gliveN, lane, geo, c.ref_fwd, c.ref_bwd, t0f, t0b);
+        if (MCM) issue_pass<CF, MCM, 0, 4, ABL>(R, gliveN, lane, geo, c.ref_fwd, c.ref_bwd, t0f, t0b);
         const Group SN = group_state<NB>(rvN, ngN);
         __builtin_amdgcn_sched_barrier(0);
         rvN = rec_load(c.mbrec, g + 2 * STEP < mb_end ? g + 2 * STEP : g, mb_last, lane);
@@ -1178,8 +1120,8 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, LT&
             // chroma taps of g+1 issued mid-iteration: spreads the wave's TA demand
             __builtin_amdgcn_sched_barrier(0);
             if (MCM) {
-                issue_pass<CF, MCM, 1, NWC, ABL>(R, gliveN, lane, geo, c.ref_fwd, c.ref_bwd, t1f, t1b);
-                if (CF != 1) issue_pass<CF, MCM, 2, NWC, ABL>(R, gliveN, lane, geo, c.ref_fwd, c.ref_bwd, t2f, t2b);
+                issue_pass<CF, MCM, 1, NWC, ABL>(R, gliveN, lane, geo, c.cref_fwd, c.cref_bwd, t1f, t1b);
+                if (CF != 1) issue_pass<CF, MCM, 2, NWC, ABL>(R, gliveN, lane, geo, c.cref_fwd, c.cref_bwd, t2f, t2b);
             }
             __builtin_amdgcn_sched_barrier(0);
             stamp<ABL>(st, 3);
@@ -1295,14 +1237,19 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, LT&
             store_pass_put8<CF, 0, 4>(gr0, glive, lane, geo, c.wsink, c.dst_slot, res8);
             store_pass_put8<CF, 1, NWC>(gr0, glive, lane, geo, c.wsink, c.dst_slot, res8);
             if (CF != 1) store_pass_put8<CF, 2, NWC>(gr0, glive, lane, geo, c.wsink, c.dst_slot, res8);
-        } else {
-            if constexpr (L2D) {  // row py = lane >> 2 of MB k = lane & 3 from the prediction image
-                const uint4 q = *(const uint4*)&L.pimg[wave][(lane & 3) * PK + (lane >> 2) * 4];
-                p0[0] = q.x, p0[1] = q.y, p0[2] = q.z, p0[3] = q.w;
+            if (c.tiles) {  // MB 0 of the group is always live
+                const uint32_t r00 = (uint32_t)__builtin_amdgcn_readfirstlane((int)gr0);
+                tile_group<CF, false>(r00 & 0xffff, r00 >> 16, lane, geo, c.wsink, c.dst_tiles, res8);
             }
-            store_pass<CF, 0, 4, ABL, MCM != 2>(gr0, gr1, glive, lane, geo, c.wsink, c.dst_slot, L.res[wave], p0);
-            store_pass<CF, 1, NWC, ABL, MCM != 2>(gr0, gr1, glive, lane, geo, c.wsink, c.dst_slot, L.res[wave], p1);
-            if (CF != 1) store_pass<CF, 2, NWC, ABL, MCM != 2>(gr0, gr1, glive, lane, geo, c.wsink, c.dst_slot, L.res[wave], p2);
+        } else {
+            store_pass<CF, 0, 4, ABL>(gr0, gr1, glive, lane, geo, c.wsink, c.dst_slot, c.dst_tiles, MCM != 2 && c.tiles, L.res[wave], p0);
+            store_pass<CF, 1, NWC, ABL>(gr0, gr1, glive, lane, geo, c.wsink, c.dst_slot, c.dst_tiles, MCM != 2 && c.tiles, L.res[wave], p1);
+            if (CF != 1) store_pass<CF, 2, NWC, ABL>(gr0, gr1, glive, lane, geo, c.wsink, c.dst_slot, c.dst_tiles, MCM != 2 && c.tiles, L.res[wave], p2);
+            if (MCM != 2 && c.tiles) {  // the pixels store_pass left in the residual image, as whole tile lines
+                wave_sync();
+                const uint32_t r00 = (uint32_t)__builtin_amdgcn_readfirstlane((int)gr0);
+                tile_group<CF, true>(r00 & 0xffff, r00 >> 16, lane, geo, c.wsink, c.dst_tiles, (const uint8_t*)L.res[wave]);
+            }
         }
         wave_sync();
 
@@ -1361,10 +1308,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MCM == 0 &&
     c.coefs = coefs;
     c.dst_slot = pool + (uint64_t)pic->dst_slot * geo.slot_stride;
     c.wsink = geo.sink + 2048 + ((b * WAVES + wave) & 1023) * 64;
-    c.ref_fwd = slot_rsrc(pool + (uint64_t)(pic->fwd_slot < 0 ? pic->dst_slot : pic->fwd_slot) * geo.slot_stride,
-                          (uint32_t)geo.slot_bytes);
-    c.ref_bwd = slot_rsrc(pool + (uint64_t)(pic->bwd_slot < 0 ? pic->dst_slot : pic->bwd_slot) * geo.slot_stride,
-                          (uint32_t)geo.slot_bytes);
+    c.dst_tiles = geo.tiles + (uint64_t)pic->dst_slot * geo.tile_stride;
+    c.tiles = sd.reserved & 1u;
+    // the taps read the references' anchor tiles (tile slot = 2 x slot bytes)
+    c.ref_fwd = slot_rsrc(geo.tiles + (uint64_t)(pic->fwd_slot < 0 ? pic->dst_slot : pic->fwd_slot) * geo.tile_stride,
+                          (uint32_t)(2 * geo.slot_bytes));
+    c.ref_bwd = slot_rsrc(geo.tiles + (uint64_t)(pic->bwd_slot < 0 ? pic->dst_slot : pic->bwd_slot) * geo.tile_stride,
+                          (uint32_t)(2 * geo.slot_bytes));
+    if (kChromaTiles) {
+        c.cref_fwd = c.ref_fwd, c.cref_bwd = c.ref_bwd;
+    } else {
+        c.cref_fwd = slot_rsrc(pool + (uint64_t)(pic->fwd_slot < 0 ? pic->dst_slot : pic->fwd_slot) * geo.slot_stride,
+                               (uint32_t)geo.slot_bytes);
+        c.cref_bwd = slot_rsrc(pool + (uint64_t)(pic->bwd_slot < 0 ? pic->dst_slot : pic->bwd_slot) * geo.slot_stride,
+                               (uint32_t)geo.slot_bytes);
+    }
     c.coef_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)coefs, (short)0, (int)kNoTap, 0x00020000);
     c.mb_begin = sd.mb_begin;
     c.mb_end = sd.mb_begin + sd.mb_count;
@@ -1442,6 +1400,8 @@ hipError_t launch_recon(int cf, int mcm, const KArgs& a, hipStream_t stream) {
     g.sink = a.sink;
     g.slot_bytes = a.slot_bytes;
     g.slot_stride = a.slot_stride;
+    g.tiles = a.tiles;
+    g.tile_stride = a.tile_stride;
     for (int i = 0; i < 3; i++) {
         g.plane_off[i] = (uint32_t)a.plane_off[i];
         g.stride[i] = a.stride[i];
@@ -1451,8 +1411,7 @@ hipError_t launch_recon(int cf, int mcm, const KArgs& a, hipStream_t stream) {
     // -DMP2VG_DEV_ABLATIONS, tools/variant.sh EXTRA=...; 4:2:0, and 16 also 4:4:4): 1 no IDCT, 2 no
     // MC, 4 no dequant, 8 no stores, 16 stage stamps (tools/stamps.py), 32 MC loads out of range
     // (no address math), 64 no prediction arithmetic, 128 no 17th-pixel dwords, 512 no edge-row
-    // loads, 1024/2048/3072 tiled / all-hit taps, 4096/8192 store shapes, 16384 anchors also store
-    // the apron-tiled copy (17408 = with the tiled taps: the whole tiled-anchor design), 32768 none.  Outputs are wrong under
+    // loads, 2048 all-hit taps, 4096/8192 store shapes, 32768 none.  Outputs are wrong under
     // it (except 16); never set in tests or the bench.  A product library refuses the variable.
     static const int ablate = getenv("MP2VG_ABLATE") ? atoi(getenv("MP2VG_ABLATE")) : 0;
 #ifndef MP2VG_DEV_ABLATIONS
@@ -1472,15 +1431,10 @@ hipError_t launch_recon(int cf, int mcm, const KArgs& a, hipStream_t stream) {
         case 96: return launch_mcm<1, 96>(mcm, a, g, stream);
         case 128: return launch_mcm<1, 128>(mcm, a, g, stream);
         case 512: return launch_mcm<1, 512>(mcm, a, g, stream);
-        case 1024: return launch_mcm<1, 1024>(mcm, a, g, stream);
-        case 1032: return launch_mcm<1, 1032>(mcm, a, g, stream);
         case 2048: return launch_mcm<1, 2048>(mcm, a, g, stream);
         case 2056: return launch_mcm<1, 2056>(mcm, a, g, stream);
-        case 3072: return launch_mcm<1, 3072>(mcm, a, g, stream);
         case 4096: return launch_mcm<1, 4096>(mcm, a, g, stream);
         case 8192: return launch_mcm<1, 8192>(mcm, a, g, stream);
-        case 16384: return launch_mcm<1, 16384>(mcm, a, g, stream);
-        case 17408: return launch_mcm<1, 17408>(mcm, a, g, stream);  // 1024 | 16384: the tiled-anchor design
         case 32768: return launch_mcm<1, 32768>(mcm, a, g, stream);  // no-op: the dev build's own baseline
         default: return hipErrorInvalidValue;
         }
@@ -1492,6 +1446,44 @@ hipError_t launch_recon(int cf, int mcm, const KArgs& a, hipStream_t stream) {
     case 3: return launch_mcm<3, 0>(mcm, a, g, stream);
     default: return hipErrorInvalidValue;
     }
+}
+
+// A slot's anchor tiles rebuilt from its frame (runtime.cpp: a batch reads a reference whose writer
+// stored no tiles -- never for an MPEG-2 stream, whose references are I/P pictures).  Thread =
+// one W-px row segment (MB column mx of row y) of one plane, stored to its two tile places.
+__global__ void __launch_bounds__(256) tile_convert_kernel(const uint8_t* __restrict__ slot, uint8_t* __restrict__ tiles,
+                                                           const Geo geo, int cw) {
+    const int plane = blockIdx.y;
+    const int w = plane == 0 ? 16 : cw;
+    const uint32_t ncol = (uint32_t)geo.stride[plane] / w, n = ncol * (uint32_t)geo.ph[plane];
+    uint8_t sink[16];
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+        const uint32_t y = i / ncol, mx = i % ncol;
+        const uint8_t* src = slot + geo.plane_off[plane] + (size_t)y * geo.stride[plane] + mx * w;
+        uint8_t* tp = tiles + 2 * (size_t)geo.plane_off[plane];
+        uint32_t out[4] = {0, 0, 0, 0};
+        if (w == 16) {
+            const uint4 v = *(const uint4*)src;
+            out[0] = v.x, out[1] = v.y, out[2] = v.z, out[3] = v.w;
+            tile_store<4>(tp, mx, y, ncol, true, sink, out);
+        } else {
+            const uint2 v = *(const uint2*)src;
+            out[0] = v.x, out[1] = v.y;
+            tile_store<2>(tp, mx, y, ncol, true, sink, out);
+        }
+    }
+}
+
+hipError_t launch_tile_convert(const uint8_t* slot, uint8_t* tiles, int cf, const KArgs& a, hipStream_t stream) {
+    Geo g;
+    for (int i = 0; i < 3; i++) {
+        g.plane_off[i] = (uint32_t)a.plane_off[i];
+        g.stride[i] = a.stride[i];
+        g.ph[i] = a.ph[i];
+    }
+    const int cw = cf == 3 ? 16 : 8;  // chroma MB width
+    hipLaunchKernelGGL(tile_convert_kernel, dim3(256, 3), dim3(256), 0, stream, slot, tiles, g, cw);
+    return hipGetLastError();
 }
 
 // Decoded slots -> the drop-in's pinned host frames (decoder.cpp), one launch per chunk: the copy

@@ -45,6 +45,8 @@ struct Geo {
     uint8_t* sink;  // 16+ writable, readable bytes outside every slot: dummy loads and stores
     uint64_t slot_bytes;   // one picture (frame_c layout): the reference rows' buffer size
     uint64_t slot_stride;  // slot i starts at pool + i * slot_stride (>= slot_bytes)
+    uint8_t* tiles;        // anchor tiles of slot i at tiles + i * tile_stride (2 x slot_bytes each)
+    uint64_t tile_stride;
     uint32_t plane_off[3];  // plane offsets inside a slot (a slot is < 4 GiB)
     int32_t stride[3];
     int32_t ph[3];
@@ -58,6 +60,8 @@ struct KArgs {
     uint8_t* pool;
     uint8_t* sink;
     uint64_t slot_bytes, slot_stride;
+    uint8_t* tiles;
+    uint64_t tile_stride;
     uint64_t plane_off[3];
     int32_t stride[3];
     int32_t ph[3];

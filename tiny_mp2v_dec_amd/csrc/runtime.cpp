@@ -20,6 +20,7 @@
 
 namespace mp2vg {
 hipError_t launch_recon(int cf, int mcm, const KArgs& a, hipStream_t stream);
+hipError_t launch_tile_convert(const uint8_t* slot, uint8_t* tiles, int cf, const KArgs& a, hipStream_t stream);
 hipError_t launch_digest(const uint8_t* pool, uint64_t slot_stride, const int32_t* d_slots, int n,
                          const uint64_t off[3], const int32_t stride[3], const int32_t w[3],
                          const int32_t h[3], unsigned long long* d_out, hipStream_t stream);
@@ -66,6 +67,21 @@ static int set_coupling() {
     return e ? atoi(e) : 0;
 }
 
+// Which pictures of a batch write anchor tiles (recon.hip tile_off: the taps read references from
+// them), decided per batch by plan_batch: a picture does when a later picture of the batch reads
+// its slot, or when it is one of the batch's last two I/P pictures (the next batch's first
+// pictures may predict from those: references are the two latest anchors, decoder.cpp:299-304).
+// A reference slot that the batch reads before writing it must hold tiles from an earlier batch;
+// when its tiles are stale (its writer did not store them) mp2vg_batch_decode rebuilds them from
+// the frame (tile_convert) on the reading set's stream first.  The kernels store tiles for I and P
+// pictures only; a B picture that a later picture reads (never in an MPEG-2 stream) gets its
+// tiles from tile_convert right after its launch.
+struct TilePlan {
+    std::vector<std::pair<int32_t, int32_t>> ext_reads;  // (slot, set) read before written
+    std::vector<std::pair<int32_t, uint8_t>> writes;     // (slot, tiles written) in decode order
+    std::vector<std::pair<int32_t, int32_t>> post;       // (launch, slot): B pictures read later
+};
+
 // One resident record batch.  The context keeps two, so the upload of batch k+1 (on the copy
 // stream) overlaps the decode of batch k; an upload waits only for the decode that last read
 // the bank it overwrites (batch k-1).
@@ -80,6 +96,7 @@ struct Bank {
     size_t cap_slices = 0;
     std::vector<Launch> launches;  // slice ranges per (dependency level, picture type)
     std::vector<std::vector<int32_t>> foot;  // per picture set: the slots it writes or reads
+    TilePlan tiles;
     int32_t npics = 0;
     hipEvent_t uploaded = nullptr;  // on ustream, after the bank's copies
     hipEvent_t consumed = nullptr;  // on stream, after the last decode that read the bank
@@ -98,6 +115,9 @@ struct mp2vg_ctx {
     uint8_t* d_pool = nullptr;
     int32_t nslots = 0;
     size_t slot_stride = 0;  // bytes from one slot to the next: the slot size plus slot_pad()
+    uint8_t* d_tiles = nullptr;  // anchor tiles of each slot (recon.hip tile_off): the taps' source
+    std::vector<uint8_t> tiles_ok;  // per slot: its tiles match its frame (after the batches enqueued)
+    size_t tile_stride = 0;      // 2 x slot bytes, 256-B aligned
     int nstreams = 2;  // independent picture sets per batch (default_streams)
 
     Bank bank[2];
@@ -179,6 +199,7 @@ extern "C" int mp2vg_create(const mp2vg_config_t* cfg, mp2vg_ctx_t** out) {
     c->cfg = *cfg;
     c->g.init(cfg->width, cfg->height, cfg->chroma_format);
     c->slot_stride = c->g.slot_bytes + slot_pad();
+    c->tile_stride = (2 * c->g.slot_bytes + 255) & ~(size_t)255;
     c->nstreams = default_streams(cfg);
     bool ok = true;
     for (Bank& b : c->bank)
@@ -218,6 +239,7 @@ extern "C" int mp2vg_destroy(mp2vg_ctx_t* c) {
         if (e) hipEventDestroy(e);
 
     hipFree(c->d_pool);
+    hipFree(c->d_tiles);
     for (Bank& b : c->bank) {
         hipFree(b.d_pics);
         hipFree(b.d_mbs);
@@ -245,7 +267,9 @@ extern "C" int mp2vg_reserve_slots(mp2vg_ctx_t* c, int32_t nslots) {
     if (nslots <= c->nslots) return MP2VG_OK;
     HIPCHK(hipStreamSynchronize(c->stream));
     uint8_t* p = nullptr;
+    uint8_t* t = nullptr;
     size_t bytes = c->slot_stride * nslots + kPoolPad;
+    const size_t tbytes = c->tile_stride * nslots;
     // dev knob for the pool-placement study (profiles/r4/README.md): 1 = physically contiguous
     // (hipDeviceMallocContiguous, default allocation if the driver refuses it)
     static const int pool_alloc = getenv("MP2VG_POOL_ALLOC") ? atoi(getenv("MP2VG_POOL_ALLOC")) : 0;
@@ -254,15 +278,24 @@ extern "C" int mp2vg_reserve_slots(mp2vg_ctx_t* c, int32_t nslots) {
         p = nullptr;
     }
     if (!p) HIPCHK(hipMalloc((void**)&p, bytes));
+    if (hipMalloc((void**)&t, tbytes) != hipSuccess) {
+        hipFree(p);
+        set_error("out of device memory for the anchor tiles");
+        return MP2VG_E_HIP;
+    }
     HIPCHK(hipMemsetAsync(p, 0, bytes, c->stream));
+    HIPCHK(hipMemsetAsync(t, 0, tbytes, c->stream));  // a never-decoded reference reads zeros, as its slot
     if (c->d_pool) {
-        HIPCHK(hipMemcpyAsync(p, c->d_pool, c->slot_stride * c->nslots, hipMemcpyDeviceToDevice,
-                              c->stream));
+        HIPCHK(hipMemcpyAsync(p, c->d_pool, c->slot_stride * c->nslots, hipMemcpyDeviceToDevice, c->stream));
+        HIPCHK(hipMemcpyAsync(t, c->d_tiles, c->tile_stride * c->nslots, hipMemcpyDeviceToDevice, c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
         HIPCHK(hipFree(c->d_pool));
+        HIPCHK(hipFree(c->d_tiles));
     }
     HIPCHK(hipStreamSynchronize(c->stream));
     c->d_pool = p;
+    c->d_tiles = t;
+    c->tiles_ok.resize(nslots, 1);  // new slots: zero frame, zero tiles
     c->nslots = nslots;
     c->last_foot.clear();  // every set of every batch is done (c->stream joined them)
     return MP2VG_OK;
@@ -272,7 +305,7 @@ extern "C" int mp2vg_reserve_slots(mp2vg_ctx_t* c, int32_t nslots) {
 static int plan_batch(mp2vg_ctx_t* c, const mp2vg_picture_t* pics, int32_t npics, const mp2vg_mb_t* mbs,
                       uint64_t nmbs, const uint32_t* coefs, uint64_t ncoefs, std::vector<SliceDesc>& slices,
                       std::vector<Launch>& launches, std::vector<std::vector<int32_t>>* foot = nullptr,
-                      bool trusted = false) {
+                      bool trusted = false, TilePlan* tplan = nullptr) {
     const int mbw = c->cfg.width / 16, mbh = c->cfg.height / 16;
     const int nb = c->g.nblocks;
     // the I kernels address coefficient words with 32-bit byte offsets (a buffer resource)
@@ -459,6 +492,31 @@ static int plan_batch(mp2vg_ctx_t* c, const mp2vg_picture_t* pics, int32_t npics
                 }
         }
     }
+    // anchor tiles (TilePlan): which pictures store them, which slots the batch reads from earlier
+    // batches, and the tiles state each written slot is left in
+    std::vector<uint8_t> need(npics, 0);
+    {
+        std::vector<int> writer(c->nslots, -1);
+        std::vector<uint8_t> ext(c->nslots, 0);
+        for (int p = 0; p < npics; p++) {
+            const mp2vg_picture_t& P = pics[p];
+            const int rs[2] = {uses_of[2 * (size_t)p] ? P.fwd_slot : -1, uses_of[2 * (size_t)p + 1] ? P.bwd_slot : -1};
+            for (int s : rs) {
+                if (s < 0) continue;
+                if (writer[s] >= 0) {
+                    need[writer[s]] = 1;
+                } else if (!ext[s]) {
+                    ext[s] = 1;
+                    if (tplan) tplan->ext_reads.push_back({s, set_of[p]});
+                }
+            }
+            writer[P.dst_slot] = p;
+        }
+        for (int p = npics - 1, anchors = 0; p >= 0 && anchors < 2; p--)
+            if (pics[p].picture_coding_type != 3) need[p] = 1, anchors++;
+        if (tplan)
+            for (int p = 0; p < npics; p++) tplan->writes.push_back({pics[p].dst_slot, need[p]});
+    }
     slices.clear();
     launches.clear();
     for (int set = 0; set < nsets; set++)
@@ -491,13 +549,18 @@ static int plan_batch(mp2vg_ctx_t* c, const mp2vg_picture_t* pics, int32_t npics
             }
             for (int r = 0; r < mbh; r++)
                 for (size_t k = i; k < j; k++)
-                    slices.push_back({(uint32_t)lp[k], pics[lp[k]].mb_first + (uint32_t)(r * mbw), (uint32_t)mbw, 0});
+                    slices.push_back({(uint32_t)lp[k], pics[lp[k]].mb_first + (uint32_t)(r * mbw), (uint32_t)mbw,
+                                      need[lp[k]]});
             i = j;
         }
         l.end = (uint32_t)slices.size();
         l.mcm = types == 1 ? 0 : (types == 2 ? 1 : (types == 4 ? 2 : 3));
         l.level = q;
         l.set = set;
+        if (tplan)
+            for (int p : lp)
+                if (need[p] && pics[p].picture_coding_type == 3)
+                    tplan->post.push_back({(int32_t)launches.size(), pics[p].dst_slot});
         launches.push_back(l);
     }
     return MP2VG_OK;
@@ -512,8 +575,9 @@ static int batch_upload(mp2vg_ctx_t* c, const mp2vg_picture_t* pics, int32_t npi
     std::vector<SliceDesc> slices;
     std::vector<Launch> lb;
     std::vector<std::vector<int32_t>> foot;
+    TilePlan tplan;
     double tp = now_ms();
-    int rc = plan_batch(c, pics, npics, mbs, nmbs, coefs, ncoefs, slices, lb, &foot, trusted);
+    int rc = plan_batch(c, pics, npics, mbs, nmbs, coefs, ncoefs, slices, lb, &foot, trusted, &tplan);
     if (rc != MP2VG_OK) return rc;
     tp = trace_phase("upload: plan", tp);
     // the other bank from the last upload; the decode queued on it is still allowed to run
@@ -539,6 +603,7 @@ static int batch_upload(mp2vg_ctx_t* c, const mp2vg_picture_t* pics, int32_t npi
     trace_phase("upload: copy", tp);
     b.launches = std::move(lb);
     b.foot = std::move(foot);
+    b.tiles = std::move(tplan);
     b.npics = npics;
     c->cur = k;
     c->batch_ready = true;
@@ -622,6 +687,8 @@ extern "C" int mp2vg_batch_decode(mp2vg_ctx_t* c) {
     a.sink = c->d_pool + c->slot_stride * c->nslots + kSinkOff;
     a.slot_bytes = c->g.slot_bytes;
     a.slot_stride = c->slot_stride;
+    a.tiles = c->d_tiles;
+    a.tile_stride = c->tile_stride;
     for (int i = 0; i < 3; i++) {
         a.plane_off[i] = c->g.plane_off[i];
         a.stride[i] = c->g.stride[i];
@@ -653,6 +720,16 @@ extern "C" int mp2vg_batch_decode(mp2vg_ctx_t* c) {
             if (overlap) HIPCHK(hipStreamWaitEvent(st, c->sev[t], 0));
         }
     }
+    // stale anchor tiles of slots this batch reads from earlier batches (rare: an MPEG-2 stream's
+    // references are anchors, which store their tiles), rebuilt on the reading set's stream
+    for (const auto& r : b.tiles.ext_reads)
+        if (r.first < c->nslots && !c->tiles_ok[r.first]) {
+            const int set = std::min(r.second, nsets - 1);
+            HIPCHK(launch_tile_convert(c->d_pool + (size_t)r.first * c->slot_stride,
+                                       c->d_tiles + (size_t)r.first * c->tile_stride, c->g.cf, a, stream_of(set)));
+            c->tiles_ok[r.first] = 1;
+        }
+    for (const auto& w : b.tiles.writes) c->tiles_ok[w.first] = w.second;
     // every set's start (after its waits): a set with no overlap with the previous batch starts
     // before set 0 does, so one start event on set 0 would under-report the batch span
     while ((int)H.s.size() < nsets) {
@@ -695,6 +772,10 @@ extern "C" int mp2vg_batch_decode(mp2vg_ctx_t* c) {
             a.nslices = launches[i].end - launches[i].begin;
             if (c->launch_timing) HIPCHK(hipEventRecord(H.l[2 * i], st));
             if (a.nslices) HIPCHK(launch_recon(c->g.cf, launches[i].mcm, a, st));
+            for (const auto& pc : b.tiles.post)  // tiles of B pictures that later pictures read
+                if (pc.first == i)
+                    HIPCHK(launch_tile_convert(c->d_pool + (size_t)pc.second * c->slot_stride,
+                                               c->d_tiles + (size_t)pc.second * c->tile_stride, c->g.cf, a, st));
             if (c->launch_timing) HIPCHK(hipEventRecord(H.l[2 * i + 1], st));
             if (couple && nsets > 1) HIPCHK(hipEventRecord(c->lev[i], st));
         }
