@@ -153,6 +153,35 @@ def test_random_records_vs_oracle(cf, big):
             assert np.array_equal(got[p][k], exp[p][k]), (p, k)
 
 
+@pytest.mark.parametrize("cf", [1, 2, 3])
+def test_anchor_tiles_across_batches(cf):
+    """The taps read references from the anchor tiles (recon.hip tile_off) that I and P pictures
+    store.  Records may also use B pictures as references (never in an MPEG-2 stream): their tiles
+    are rebuilt from the frame, inside a batch right after the B picture's launch, and across
+    batches when a batch reads a slot whose last writer stored none (runtime.cpp TilePlan).  Two
+    batches, pictures 0-2 then 3-4: picture 3 reads B picture 2 of the first batch, picture 4
+    reads B pictures 3 and 2; every frame vs the oracle."""
+    w, h = 96, 64
+    pics, mbs, coefs = random_batch(w, h, cf, 5, seed=4242 + cf)
+    exp = oracle_frames(_P(w, h, cf, pics, mbs, coefs))
+    n = (w // 16) * (h // 16)
+    c0 = int(mbs["coef_off"][3 * n])
+    p2 = pics[3:].copy()
+    p2["mb_first"] -= 3 * n
+    m2 = mbs[3 * n:].copy()
+    m2["coef_off"] -= c0
+    with R.DeviceContext(w, h, cf, slots=5) as ctx:
+        ctx.upload(pics[:3], mbs[:3 * n], coefs[:c0])
+        ctx.decode()
+        ctx.upload(p2, m2, coefs[c0:])
+        ctx.decode()
+        ctx.synchronize()
+        for p in range(5):
+            got = ctx.download(p)
+            for k in range(3):
+                assert np.array_equal(got[k], exp[p][k]), (p, k)
+
+
 def test_full_size_1080p_digest_vs_oracle():
     """BASELINE config size (1920x1088 4:2:0, one closed GOP of the §8d C2 mix): device digest of
     every frame == host digest of the oracle's frames (size-independent checksum-of-checksums)."""

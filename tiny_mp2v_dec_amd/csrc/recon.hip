@@ -510,6 +510,25 @@ __device__ __forceinline__ void issue_pass(const LaneRec& L, bool live, int lane
                                    (fl >> (9 + 2 * r)) & 1, stride, ph);
 }
 
+// The frame_c rows: no kernel reads them back (the taps read the anchor tiles), so they can be
+// stored nontemporally (MP2VG_NT_ROWS: dev A/B) and leave L2 to the tiles and the references
+#ifndef MP2VG_NT_ROWS
+#define MP2VG_NT_ROWS 0
+#endif
+typedef uint32_t u2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void row_store16(uint8_t* d, uint32_t a, uint32_t b, uint32_t c, uint32_t e) {
+    if (MP2VG_NT_ROWS)
+        __builtin_nontemporal_store(u4v{a, b, c, e}, (u4v*)d);
+    else
+        *(uint4*)d = make_uint4(a, b, c, e);
+}
+__device__ __forceinline__ void row_store8(uint8_t* d, uint32_t a, uint32_t b) {
+    if (MP2VG_NT_ROWS)
+        __builtin_nontemporal_store(u2v{a, b}, (u2v*)d);
+    else
+        *(uint2*)d = make_uint2(a, b);
+}
+
 // ---- add/clip + store ----------------------------------------------------------------------
 // An anchor row's two tile copies (tile_off): its own tile and the apron of the tile to its left
 // (MB column 0 has none).  Dead lanes write the wave's sink line.
@@ -590,9 +609,9 @@ __device__ __forceinline__ void store_pass(uint32_t r0, uint32_t r1, bool live, 
         asm volatile("" ::"v"(out[0]), "v"(out[1]), "v"(out[2]), "v"(out[3]));
         *(uint32_t*)dst = out[0] ^ out[1] ^ (NW == 4 ? out[2] ^ out[3] : 0u);
     } else if (NW == 4) {
-        *(uint4*)dst = make_uint4(out[0], out[1], out[2], out[3]);
+        row_store16(dst, out[0], out[1], out[2], out[3]);
     } else {
-        *(uint2*)dst = make_uint2(out[0], out[1]);
+        row_store8(dst, out[0], out[1]);
     }
 }
 
@@ -613,11 +632,11 @@ __device__ __forceinline__ void store_pass_put8(uint32_t r0, bool live, int lane
     dst = live ? dst : wsink;  // branch-free: every lane stores (see Tap)
     if (NW == 4) {
         const uint4 q = *(const uint4*)row;
-        *(uint4*)dst = make_uint4(__builtin_amdgcn_perm(q.x, q.x, 0x03010200u), __builtin_amdgcn_perm(q.y, q.y, 0x03010200u),
+        row_store16(dst, __builtin_amdgcn_perm(q.x, q.x, 0x03010200u), __builtin_amdgcn_perm(q.y, q.y, 0x03010200u),
                                   __builtin_amdgcn_perm(q.z, q.z, 0x03010200u), __builtin_amdgcn_perm(q.w, q.w, 0x03010200u));
     } else {
         const uint2 q = *(const uint2*)row;
-        *(uint2*)dst = make_uint2(__builtin_amdgcn_perm(q.x, q.x, 0x03010200u), __builtin_amdgcn_perm(q.y, q.y, 0x03010200u));
+        row_store8(dst, __builtin_amdgcn_perm(q.x, q.x, 0x03010200u), __builtin_amdgcn_perm(q.y, q.y, 0x03010200u));
     }
 }
 
@@ -648,7 +667,7 @@ __device__ __forceinline__ uint2 img_row8(const uint8_t* img, int k, int plane, 
     const uint2 q = *(const uint2*)img_row<CF, NAT>(img, k, plane, py);
     return make_uint2(unswz(q.x, NAT), unswz(q.y, NAT));
 }
-template <int CF, bool NAT>
+template <int CF, bool NAT, int ABL = 0>
 __device__ __forceinline__ void tile_group(uint32_t mx0, uint32_t mby, int lane, const Geo& geo, uint8_t* wsink,
                                            uint8_t* dst_tiles, const uint8_t* res8) {
     using F = Fmt<CF>;
@@ -669,7 +688,7 @@ __device__ __forceinline__ void tile_group(uint32_t mx0, uint32_t mby, int lane,
             const uint4 v = img_row16<CF, NAT>(res8, j + h, plane, r);
             const bool none = j < 0 && mx0 == 0;
             const uint32_t o = tile_row<16>(mx0 + (uint32_t)j, mby * 16u + (uint32_t)r, ncol) + (uint32_t)h * 16u;
-            *(uint4*)(none ? wsink : tp + o) = v;
+            *(uint4*)(none ? wsink : ((ABL & 65536) ? dst_tiles + (o & 0xFFF0u) : tp + o)) = v;
         }
     }
     if constexpr (CF != 3 && kChromaTiles) {  // W-8 chroma: Cb and Cr
@@ -683,7 +702,8 @@ __device__ __forceinline__ void tile_group(uint32_t mx0, uint32_t mby, int lane,
             const int j = rem / RPM, r = rem % RPM;
             const uint2 a = img_row8<CF, NAT>(res8, j, plane, r), b = img_row8<CF, NAT>(res8, min(j + 1, 3), plane, r);
             const uint32_t o = tile_row<8>(mx0 + (uint32_t)j, mby * (uint32_t)RPM + (uint32_t)r, ncol);
-            *(uint4*)(u < N16 ? dst_tiles + 2u * gsel(geo.plane_off, plane) + o : wsink) = make_uint4(a.x, a.y, b.x, b.y);
+            uint8_t* d = (ABL & 65536) ? dst_tiles + (o & 0xFFF0u) : dst_tiles + 2u * gsel(geo.plane_off, plane) + o;
+            *(uint4*)(u < N16 ? d : wsink) = make_uint4(a.x, a.y, b.x, b.y);
         }
 #pragma nounroll
         for (int i = 0; i < (N8 + 63) / 64; i++) {
@@ -694,7 +714,8 @@ __device__ __forceinline__ void tile_group(uint32_t mx0, uint32_t mby, int lane,
             const uint2 v = img_row8<CF, NAT>(res8, side ? 0 : 3, plane, r);
             const uint32_t o = tile_row<8>(mx0 + (uint32_t)j, mby * (uint32_t)RPM + (uint32_t)r, ncol) + (uint32_t)h * 8u;
             const bool none = u >= N8 || (side && mx0 == 0);
-            *(uint2*)(none ? wsink : dst_tiles + 2u * gsel(geo.plane_off, plane) + o) = v;
+            uint8_t* d = (ABL & 65536) ? dst_tiles + (o & 0xFFF8u) : dst_tiles + 2u * gsel(geo.plane_off, plane) + o;
+            *(uint2*)(none ? wsink : d) = v;
         }
     }
 }
@@ -1239,7 +1260,7 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, LT&
             if (CF != 1) store_pass_put8<CF, 2, NWC>(gr0, glive, lane, geo, c.wsink, c.dst_slot, res8);
             if (c.tiles) {  // MB 0 of the group is always live
                 const uint32_t r00 = (uint32_t)__builtin_amdgcn_readfirstlane((int)gr0);
-                tile_group<CF, false>(r00 & 0xffff, r00 >> 16, lane, geo, c.wsink, c.dst_tiles, res8);
+                tile_group<CF, false, ABL>(r00 & 0xffff, r00 >> 16, lane, geo, c.wsink, c.dst_tiles, res8);
             }
         } else {
             store_pass<CF, 0, 4, ABL>(gr0, gr1, glive, lane, geo, c.wsink, c.dst_slot, c.dst_tiles, MCM != 2 && c.tiles, L.res[wave], p0);
@@ -1248,7 +1269,7 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, LT&
             if (MCM != 2 && c.tiles) {  // the pixels store_pass left in the residual image, as whole tile lines
                 wave_sync();
                 const uint32_t r00 = (uint32_t)__builtin_amdgcn_readfirstlane((int)gr0);
-                tile_group<CF, true>(r00 & 0xffff, r00 >> 16, lane, geo, c.wsink, c.dst_tiles, (const uint8_t*)L.res[wave]);
+                tile_group<CF, true, ABL>(r00 & 0xffff, r00 >> 16, lane, geo, c.wsink, c.dst_tiles, (const uint8_t*)L.res[wave]);
             }
         }
         wave_sync();
@@ -1267,16 +1288,20 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, LT&
     }
 }
 
+// dev ablations that keep the I kernels' compact layout: 16 stamps, 32768 none, 65536 tile stores
+// into a 64-KB window of the tile slot (L2-resident: the stores' memory traffic, not their issue)
+constexpr int kAblCompact = 16 | 32768 | 65536;
+
 // Occupancy targets per kernel from its LDS: 4:2:0 / 4:2:2 P/B workgroups fit 4 per CU (128
 // VGPRs), 4:4:4 P/B 3 (168 VGPRs cost nothing); the compact I kernels fit 4 (4:4:4) or 6 (80 VGPRs)
 template <int CF, int MCM, int ABL = 0>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MCM == 0 && ABL == 0 ? (CF == 3 ? 4 : 6) : (CF == 3 ? 3 : 4)))) void recon_kernel(const mp2vg_picture_t* __restrict__ pics,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MCM == 0 && (ABL & ~kAblCompact) == 0 ? (CF == 3 ? 4 : 6) : (CF == 3 ? 3 : 4)))) void recon_kernel(const mp2vg_picture_t* __restrict__ pics,
                                                     const uint32_t* __restrict__ mbrec,
                                                     const uint32_t* __restrict__ coefs,
                                                     const SliceDesc* __restrict__ slices,
                                                     uint8_t* __restrict__ pool, const Geo geo,
                                                     const uint32_t slice_base, const uint32_t nslices) {
-    using LT = Lds<CF, MCM == 0 && ABL == 0>;
+    using LT = Lds<CF, MCM == 0 && (ABL & ~kAblCompact) == 0>;
     __shared__ __attribute__((aligned(128))) LT L;  // 128-B aligned: pass1_store
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -1436,6 +1461,7 @@ hipError_t launch_recon(int cf, int mcm, const KArgs& a, hipStream_t stream) {
         case 4096: return launch_mcm<1, 4096>(mcm, a, g, stream);
         case 8192: return launch_mcm<1, 8192>(mcm, a, g, stream);
         case 32768: return launch_mcm<1, 32768>(mcm, a, g, stream);  // no-op: the dev build's own baseline
+        case 65536: return launch_mcm<1, 65536>(mcm, a, g, stream);  // tile stores in a 64-KB window
         default: return hipErrorInvalidValue;
         }
     }

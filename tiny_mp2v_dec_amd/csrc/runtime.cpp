@@ -62,6 +62,10 @@ static size_t slot_pad() {
     const char* e = getenv("MP2VG_SLOT_PAD");
     return e ? (size_t)std::max(0, atoi(e)) & ~(size_t)255 : 0;
 }
+static size_t tile_pad() {  // the same for the anchor-tile slots (MP2VG_TILE_PAD)
+    const char* e = getenv("MP2VG_TILE_PAD");
+    return e ? (size_t)std::max(0, atoi(e)) & ~(size_t)255 : 0;
+}
 static int set_coupling() {
     const char* e = getenv("MP2VG_SET_COUPLE");
     return e ? atoi(e) : 0;
@@ -199,7 +203,7 @@ extern "C" int mp2vg_create(const mp2vg_config_t* cfg, mp2vg_ctx_t** out) {
     c->cfg = *cfg;
     c->g.init(cfg->width, cfg->height, cfg->chroma_format);
     c->slot_stride = c->g.slot_bytes + slot_pad();
-    c->tile_stride = (2 * c->g.slot_bytes + 255) & ~(size_t)255;
+    c->tile_stride = ((2 * c->g.slot_bytes + 255) & ~(size_t)255) + tile_pad();
     c->nstreams = default_streams(cfg);
     bool ok = true;
     for (Bank& b : c->bank)
@@ -277,9 +281,18 @@ extern "C" int mp2vg_reserve_slots(mp2vg_ctx_t* c, int32_t nslots) {
         (void)hipGetLastError();
         p = nullptr;
     }
+    // 2 = the pool and tiles allocated while a same-size block is held (freed after), 3 = after
+    // such a block was allocated and freed: is the placement of a process's first big allocation
+    // the slow one (profiles/r4/README.md)?
+    uint8_t* dummy = nullptr;
+    if (pool_alloc == 2 || pool_alloc == 3) {
+        if (hipMalloc((void**)&dummy, bytes + tbytes) != hipSuccess) (void)hipGetLastError(), dummy = nullptr;
+        if (dummy && pool_alloc == 3) hipFree(dummy), dummy = nullptr;
+    }
     if (!p) HIPCHK(hipMalloc((void**)&p, bytes));
     if (hipMalloc((void**)&t, tbytes) != hipSuccess) {
         hipFree(p);
+        if (dummy) hipFree(dummy);
         set_error("out of device memory for the anchor tiles");
         return MP2VG_E_HIP;
     }
@@ -293,6 +306,7 @@ extern "C" int mp2vg_reserve_slots(mp2vg_ctx_t* c, int32_t nslots) {
         HIPCHK(hipFree(c->d_tiles));
     }
     HIPCHK(hipStreamSynchronize(c->stream));
+    if (dummy) hipFree(dummy);
     c->d_pool = p;
     c->d_tiles = t;
     c->tiles_ok.resize(nslots, 1);  // new slots: zero frame, zero tiles
