@@ -138,13 +138,12 @@ def picture_taps(P, mbs, stride, ph, plane_off, cf, layout, luma=True):
                     if layout == "linear":
                         a = plane_off[plane] + rows * st + X0
                         spans = [(a, a + min(nbytes, 16) - 1, 0)] + ([(a + 16, a + nbytes - 1, 1)] if nbytes > 16 else [])
-                    elif layout == "apron":  # one load per row inside a tile row with its apron
-                        if plane == 0:
-                            t = (rows >> 2) * (st // 16) + (X0 >> 4)
-                            a = t * 128 + (rows & 3) * 32 + (X0 & 15)
-                        else:
-                            t = (rows >> 3) * (st // 8) + (X0 >> 3)
-                            a = (1 << 40) * plane + t * 128 + (rows & 7) * 16 + (X0 & 7)
+                    elif layout.startswith("apron"):  # one load per row inside a tile row with its apron
+                        # apron: 4 rows x (16 + 16 apron) luma, 8 x (8 + 8) chroma (recon.hip tile_off);
+                        # apron2: 2 rows x (48 + 16 apron) luma, 4 x (24 + 8) chroma (1.33x the bytes)
+                        R_, OW = ((4, 16), (8, 8)) [plane > 0] if layout == "apron" else ((2, 48), (4, 24))[plane > 0]
+                        t = (rows // R_) * -(-st // OW) + (X0 // OW)
+                        a = (1 << 40) * plane + t * 128 + (rows % R_) * (128 // R_) + (X0 % OW)
                         spans = [(a, a + min(nbytes, 16) - 1, 0)] + ([(a + 16, a + nbytes - 1, 1)] if nbytes > 16 else [])
                     else:  # tile8x16: two loads per row (the row's left tile, then its right tile)
                         tw = 16 if plane == 0 else 16
@@ -176,7 +175,7 @@ def main():
     plane_off = [0, stride[0] * ph[0], stride[0] * ph[0] + stride[1] * ph[1]]
     n = int(parsed.pics[0]["mb_width"]) * int(parsed.pics[0]["mb_height"])
     res = {}
-    for layout in ("linear", "apron", "tile8x16", "luma2d_tw8", "luma2d_tw4"):
+    for layout in ("linear", "apron", "apron2", "tile8x16", "luma2d_tw8", "luma2d_tw4"):
         ta_l = ta_s = grp_l = groups = 0
         for p in range(parsed.npics):
             P = parsed.pics[p]

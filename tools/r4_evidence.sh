@@ -28,6 +28,10 @@ for c in ${CONFIGS:-c1 c3 c4 c5}; do
   timeout -k 10 400 python bench.py $extra --config $c > $OUT/bench_$c.json 2> $OUT/bench_$c.err || { tail -5 $OUT/bench_$c.err; exit 1; }
   echo "$c: $(tail -1 $OUT/bench_$c.json | head -c 200)"
 done
+if [ "${E2E1:-1}" = 1 ]; then  # the drop-in and the reference at one host thread (verdict r3 item 6)
+  timeout -k 10 600 python tools/e2e_bench.py --threads 1 --ref --gops 8 > $OUT/e2e_1thread.json 2> $OUT/e2e_1thread.err || { tail -5 $OUT/e2e_1thread.err; exit 1; }
+  echo "e2e 1 thread: $(tail -1 $OUT/e2e_1thread.json)"
+fi
 for c in ${PROFILE:-c2 c5}; do
   PASSES=traffic tools/profile.sh ${TAG}_$c --config $c --steps 10 --warmup 2 --no-e2e > $OUT/profile_$c.log 2>&1 || { cat $OUT/profile_$c.log; exit 1; }
   echo "profile $c ok"
