@@ -237,8 +237,9 @@ extern "C" int mp2vg_decoder_create_multi(const mp2vg_config_t* cfg, const int32
     d->user = user;
     d->g.init(cfg->width, cfg->height, cfg->chroma_format);
     d->device_frames = cfg->reserved & MP2VG_DECODER_DEVICE_FRAMES;
-    d->kernel_copy = kDlKernel && !d->device_frames;
-    for (int i = 1; i < ndevices; i++) d->kernel_copy = d->kernel_copy && devices[i] == devices[0];
+    // the copy kernel: into pinned host frames (one device), or into each lane's own HBM frames
+    d->kernel_copy = kDlKernel;
+    for (int i = 1; i < ndevices; i++) d->kernel_copy = d->kernel_copy && (d->device_frames || devices[i] == devices[0]);
     // frames in flight per lane: one chunk being copied, one being rendered, anchors held for display
     const int frames_per_lane = 2 * kChunk + 4;
     const size_t chunk_mbs = (size_t)kChunk * (cfg->width / 16) * (cfg->height / 16);
@@ -572,9 +573,10 @@ extern "C" int mp2vg_decoder_decode(mp2vg_decoder_t* d, const uint8_t* buf, uint
             hipSetDevice(L.device);
             // the pinned frame as this device addresses it (a frame the device cannot map goes
             // by DMA)
-            void* hdst = nullptr;
+            // (device frames: the frame itself, in HBM on this lane's device)
+            void* hdst = d->device_frames ? (void*)hf->data : nullptr;
             const bool by_kernel = d->kernel_copy &&
-                                   hipHostGetDevicePointer(&hdst, hf->data, 0) == hipSuccess &&
+                                   (d->device_frames || hipHostGetDevicePointer(&hdst, hf->data, 0) == hipSuccess) &&
                                    !(((uintptr_t)hdst | (uintptr_t)src) & 15);
             if (rc == MP2VG_OK && by_kernel) {
                 fc.src[nfc] = (const uint8_t*)src;

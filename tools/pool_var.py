@@ -27,8 +27,10 @@ def timed(ctx):
         ctx.decode()
     ctx.synchronize()
     ms = (time.perf_counter() - t0) * 1e3 / steps
-    launch = sum(sum(ctx.batch_times(b)[1]) for b in range(steps)) / steps
-    return ms, launch
+    per = [ctx.batch_times(b)[1] for b in range(steps)]
+    launch = sum(sum(x) for x in per) / steps
+    each = [sum(x[i] for x in per) / steps for i in range(len(per[0]))]  # per launch (I, P+B, B+P, B+P, B)
+    return ms, launch, each
 
 
 for t in range(trials):
@@ -39,7 +41,8 @@ for t in range(trials):
         ctxs.append(c)
     for rep in range(2):
         for name, c in zip("AB", ctxs):
-            ms, launch = timed(c)
-            print(f"trial {t} ctx {name} rep {rep}: {ms:.3f} ms/step, launches {launch:.3f} ms/step", flush=True)
+            ms, launch, each = timed(c)
+            print(f"trial {t} ctx {name} rep {rep}: {ms:.3f} ms/step, launches {launch:.3f} ms/step "
+                  f"({' '.join(f'{x:.3f}' for x in each)})", flush=True)
     for c in ctxs:
         c.close()
