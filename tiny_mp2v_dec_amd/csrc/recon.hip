@@ -1299,7 +1299,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MCM == 0 &&
                                                     const uint32_t* __restrict__ mbrec,
                                                     const uint32_t* __restrict__ coefs,
                                                     const SliceDesc* __restrict__ slices,
-                                                    uint8_t* __restrict__ pool, const Geo geo,
+                                                    const Geo geo,
                                                     const uint32_t slice_base, const uint32_t nslices) {
     using LT = Lds<CF, MCM == 0 && (ABL & ~kAblCompact) == 0>;
     __shared__ __attribute__((aligned(128))) LT L;  // 128-B aligned: pass1_store
@@ -1331,22 +1331,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MCM == 0 &&
     SliceCtx c;
     c.mbrec = mbrec;
     c.coefs = coefs;
-    c.dst_slot = pool + (uint64_t)pic->dst_slot * geo.slot_stride;
+    c.dst_slot = (uint8_t*)geo.ftab[pic->dst_slot];
     c.wsink = geo.sink + 2048 + ((b * WAVES + wave) & 1023) * 64;
-    c.dst_tiles = geo.tiles + (uint64_t)pic->dst_slot * geo.tile_stride;
+    c.dst_tiles = (uint8_t*)geo.ttab[pic->dst_slot];
     c.tiles = sd.reserved & 1u;
     // the taps read the references' anchor tiles (tile slot = 2 x slot bytes)
-    c.ref_fwd = slot_rsrc(geo.tiles + (uint64_t)(pic->fwd_slot < 0 ? pic->dst_slot : pic->fwd_slot) * geo.tile_stride,
-                          (uint32_t)(2 * geo.slot_bytes));
-    c.ref_bwd = slot_rsrc(geo.tiles + (uint64_t)(pic->bwd_slot < 0 ? pic->dst_slot : pic->bwd_slot) * geo.tile_stride,
-                          (uint32_t)(2 * geo.slot_bytes));
+    const int fs = pic->fwd_slot < 0 ? pic->dst_slot : pic->fwd_slot;
+    const int bs = pic->bwd_slot < 0 ? pic->dst_slot : pic->bwd_slot;
+    c.ref_fwd = slot_rsrc((const uint8_t*)geo.ttab[fs], (uint32_t)(2 * geo.slot_bytes));
+    c.ref_bwd = slot_rsrc((const uint8_t*)geo.ttab[bs], (uint32_t)(2 * geo.slot_bytes));
     if (kChromaTiles) {
         c.cref_fwd = c.ref_fwd, c.cref_bwd = c.ref_bwd;
     } else {
-        c.cref_fwd = slot_rsrc(pool + (uint64_t)(pic->fwd_slot < 0 ? pic->dst_slot : pic->fwd_slot) * geo.slot_stride,
-                               (uint32_t)geo.slot_bytes);
-        c.cref_bwd = slot_rsrc(pool + (uint64_t)(pic->bwd_slot < 0 ? pic->dst_slot : pic->bwd_slot) * geo.slot_stride,
-                               (uint32_t)geo.slot_bytes);
+        c.cref_fwd = slot_rsrc((const uint8_t*)geo.ftab[fs], (uint32_t)geo.slot_bytes);
+        c.cref_bwd = slot_rsrc((const uint8_t*)geo.ftab[bs], (uint32_t)geo.slot_bytes);
     }
     c.coef_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)coefs, (short)0, (int)kNoTap, 0x00020000);
     c.mb_begin = sd.mb_begin;
@@ -1373,11 +1371,11 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
     return z ^ (z >> 31);
 }
 
-__global__ void digest_kernel(const uint8_t* __restrict__ pool, uint64_t slot_stride, const int32_t* __restrict__ slots,
+__global__ void digest_kernel(const uint64_t* __restrict__ ftab, const int32_t* __restrict__ slots,
                               uint64_t o0, uint64_t o1, uint64_t o2, int s0, int s1, int w0, int w1, int h0, int h1,
                               unsigned long long* __restrict__ out) {
     const int si = blockIdx.y;
-    const uint8_t* base = pool + (uint64_t)slots[si] * slot_stride;
+    const uint8_t* base = (const uint8_t*)ftab[slots[si]];
     const int rows = h0 + 2 * h1;
     uint64_t acc = 0;
     for (int row = blockIdx.x; row < rows; row += gridDim.x) {
@@ -1405,7 +1403,7 @@ __global__ void digest_kernel(const uint8_t* __restrict__ pool, uint64_t slot_st
 template <int CF, int MCM, int ABL>
 static void launch_one(const KArgs& a, const Geo& g, hipStream_t stream) {
     hipLaunchKernelGGL((recon_kernel<CF, MCM, ABL>), dim3(a.nslices), dim3(256), 0, stream, a.pics,
-                       (const uint32_t*)a.mbs, a.coefs, a.slices, a.pool, g, a.slice_base, a.nslices);
+                       (const uint32_t*)a.mbs, a.coefs, a.slices, g, a.slice_base, a.nslices);
 }
 
 template <int CF, int ABL>
@@ -1424,9 +1422,8 @@ hipError_t launch_recon(int cf, int mcm, const KArgs& a, hipStream_t stream) {
     Geo g;
     g.sink = a.sink;
     g.slot_bytes = a.slot_bytes;
-    g.slot_stride = a.slot_stride;
-    g.tiles = a.tiles;
-    g.tile_stride = a.tile_stride;
+    g.ftab = a.ftab;
+    g.ttab = a.ttab;
     for (int i = 0; i < 3; i++) {
         g.plane_off[i] = (uint32_t)a.plane_off[i];
         g.stride[i] = a.stride[i];
@@ -1540,11 +1537,11 @@ hipError_t launch_frame_copy(const FrameCopy& fc, int n, uint64_t bytes, hipStre
     return hipGetLastError();
 }
 
-hipError_t launch_digest(const uint8_t* pool, uint64_t slot_stride, const int32_t* d_slots, int n,
+hipError_t launch_digest(const uint64_t* ftab, const int32_t* d_slots, int n,
                          const uint64_t off[3], const int32_t stride[3], const int32_t w[3],
                          const int32_t h[3], unsigned long long* d_out, hipStream_t stream) {
     dim3 block(256), grid(64, n);
-    hipLaunchKernelGGL(digest_kernel, grid, block, 0, stream, pool, slot_stride, d_slots, off[0], off[1], off[2],
+    hipLaunchKernelGGL(digest_kernel, grid, block, 0, stream, ftab, d_slots, off[0], off[1], off[2],
                        stride[0], stride[1], w[0], w[1], h[0], h[1], d_out);
     return hipGetLastError();
 }

@@ -43,10 +43,9 @@ struct Launch {
 // per-launch geometry, passed by value
 struct Geo {
     uint8_t* sink;  // 16+ writable, readable bytes outside every slot: dummy loads and stores
-    uint64_t slot_bytes;   // one picture (frame_c layout): the reference rows' buffer size
-    uint64_t slot_stride;  // slot i starts at pool + i * slot_stride (>= slot_bytes)
-    uint8_t* tiles;        // anchor tiles of slot i at tiles + i * tile_stride (2 x slot_bytes each)
-    uint64_t tile_stride;
+    uint64_t slot_bytes;   // one picture (frame_c layout); a slot's anchor tiles are 2 x this
+    const uint64_t* ftab;  // device address of frame slot i (the frame pool's slot table)
+    const uint64_t* ttab;  // device address of slot i's anchor tiles
     uint32_t plane_off[3];  // plane offsets inside a slot (a slot is < 4 GiB)
     int32_t stride[3];
     int32_t ph[3];
@@ -57,11 +56,9 @@ struct KArgs {
     const mp2vg_mb_t* mbs;
     const uint32_t* coefs;
     const SliceDesc* slices;
-    uint8_t* pool;
     uint8_t* sink;
-    uint64_t slot_bytes, slot_stride;
-    uint8_t* tiles;
-    uint64_t tile_stride;
+    uint64_t slot_bytes;
+    const uint64_t *ftab, *ttab;
     uint64_t plane_off[3];
     int32_t stride[3];
     int32_t ph[3];

@@ -21,7 +21,7 @@
 namespace mp2vg {
 hipError_t launch_recon(int cf, int mcm, const KArgs& a, hipStream_t stream);
 hipError_t launch_tile_convert(const uint8_t* slot, uint8_t* tiles, int cf, const KArgs& a, hipStream_t stream);
-hipError_t launch_digest(const uint8_t* pool, uint64_t slot_stride, const int32_t* d_slots, int n,
+hipError_t launch_digest(const uint64_t* ftab, const int32_t* d_slots, int n,
                          const uint64_t off[3], const int32_t stride[3], const int32_t w[3],
                          const int32_t h[3], unsigned long long* d_out, hipStream_t stream);
 }  // namespace mp2vg
@@ -116,10 +116,16 @@ struct mp2vg_ctx {
     std::vector<hipEvent_t> sev;        // end of each set's launches in the last batch
     std::vector<hipEvent_t> lev;        // end of each launch of the current batch (set coupling)
     std::vector<std::vector<uint8_t>> last_foot;  // slots each set of the last batch touched
-    uint8_t* d_pool = nullptr;
+    uint8_t* d_pool = nullptr;   // the frame slots in one block (null with MP2VG_POOL_CHUNK)
     int32_t nslots = 0;
     size_t slot_stride = 0;  // bytes from one slot to the next: the slot size plus slot_pad()
     uint8_t* d_tiles = nullptr;  // anchor tiles of each slot (recon.hip tile_off): the taps' source
+    // per-slot device addresses of the frame and of its tiles (host copies, and the table the
+    // kernels index: [frames | tiles]); chunked pools (MP2VG_POOL_CHUNK slots per block) add blocks
+    std::vector<uint64_t> fptr, tptr;
+    std::vector<uint8_t*> chunks;
+    uint64_t* d_tab = nullptr;
+    uint8_t* d_sink = nullptr;   // dummy loads / stores of the kernels (kPoolPad bytes)
     std::vector<uint8_t> tiles_ok;  // per slot: its tiles match its frame (after the batches enqueued)
     size_t tile_stride = 0;      // 2 x slot bytes, 256-B aligned
     int nstreams = 2;  // independent picture sets per batch (default_streams)
@@ -244,6 +250,9 @@ extern "C" int mp2vg_destroy(mp2vg_ctx_t* c) {
 
     hipFree(c->d_pool);
     hipFree(c->d_tiles);
+    for (auto q : c->chunks) hipFree(q);
+    hipFree(c->d_tab);
+    hipFree(c->d_sink);
     for (Bank& b : c->bank) {
         hipFree(b.d_pics);
         hipFree(b.d_mbs);
@@ -265,11 +274,54 @@ extern "C" int mp2vg_destroy(mp2vg_ctx_t* c) {
     return MP2VG_OK;
 }
 
+// the slot table the kernels index ([frame addresses | tile addresses]) and the slot state
+static int finish_reserve(mp2vg_ctx_t* c, int32_t nslots) {
+    hipFree(c->d_tab);
+    c->d_tab = nullptr;
+    HIPCHK(hipMalloc((void**)&c->d_tab, sizeof(uint64_t) * 2 * nslots));
+    HIPCHK(hipMemcpyAsync(c->d_tab, c->fptr.data(), sizeof(uint64_t) * nslots, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(c->d_tab + nslots, c->tptr.data(), sizeof(uint64_t) * nslots, hipMemcpyHostToDevice,
+                          c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    c->tiles_ok.resize(nslots, 1);  // new slots: zero frame, zero tiles
+    c->nslots = nslots;
+    c->last_foot.clear();  // every set of every batch is done (c->stream joined them)
+    return MP2VG_OK;
+}
+
 extern "C" int mp2vg_reserve_slots(mp2vg_ctx_t* c, int32_t nslots) {
     if (!c || nslots <= 0) return MP2VG_E_INVALID;
     HIPCHK(hipSetDevice(c->cfg.device));
     if (nslots <= c->nslots) return MP2VG_OK;
     HIPCHK(hipStreamSynchronize(c->stream));
+    if (!c->d_sink) {
+        HIPCHK(hipMalloc((void**)&c->d_sink, kPoolPad));
+        HIPCHK(hipMemsetAsync(c->d_sink, 0, kPoolPad, c->stream));
+    }
+    // The slots come in blocks of 16 (MP2VG_POOL_CHUNK; 0 = one block for all), each block its own
+    // allocation (frames, then tiles), added as the pool grows (no copy).  One pool-sized
+    // allocation lands, in some processes, where the anchors' tile stores run 10-20 % slower
+    // (c2 334.8k vs 365.4k frames/s, same library and box); blocks of 16 slots measured 349.4k /
+    // 349.6k against 322.8k / 322.8k for one block on a box where the single block was slow
+    // (profiles/r4/README.md, placement).
+    static const int chunk = getenv("MP2VG_POOL_CHUNK") ? std::max(0, atoi(getenv("MP2VG_POOL_CHUNK"))) : 16;
+    if (chunk > 0) {
+        for (int s0 = c->nslots; s0 < nslots; s0 += chunk) {
+            const int k = std::min(chunk, nslots - s0);
+            uint8_t *f = nullptr, *t = nullptr;
+            HIPCHK(hipMalloc((void**)&f, c->slot_stride * k + kPoolPad));
+            c->chunks.push_back(f);
+            HIPCHK(hipMalloc((void**)&t, c->tile_stride * k));
+            c->chunks.push_back(t);
+            HIPCHK(hipMemsetAsync(f, 0, c->slot_stride * k + kPoolPad, c->stream));
+            HIPCHK(hipMemsetAsync(t, 0, c->tile_stride * k, c->stream));
+            for (int i = 0; i < k; i++) {
+                c->fptr.push_back((uint64_t)(uintptr_t)(f + (size_t)i * c->slot_stride));
+                c->tptr.push_back((uint64_t)(uintptr_t)(t + (size_t)i * c->tile_stride));
+            }
+        }
+        return finish_reserve(c, nslots);
+    }
     uint8_t* p = nullptr;
     uint8_t* t = nullptr;
     size_t bytes = c->slot_stride * nslots + kPoolPad;
@@ -315,10 +367,13 @@ extern "C" int mp2vg_reserve_slots(mp2vg_ctx_t* c, int32_t nslots) {
     if (dummy) hipFree(dummy);
     c->d_pool = p;
     c->d_tiles = t;
-    c->tiles_ok.resize(nslots, 1);  // new slots: zero frame, zero tiles
-    c->nslots = nslots;
-    c->last_foot.clear();  // every set of every batch is done (c->stream joined them)
-    return MP2VG_OK;
+    c->fptr.resize(nslots);
+    c->tptr.resize(nslots);
+    for (int i = 0; i < nslots; i++) {
+        c->fptr[i] = (uint64_t)(uintptr_t)(p + (size_t)i * c->slot_stride);
+        c->tptr[i] = (uint64_t)(uintptr_t)(t + (size_t)i * c->tile_stride);
+    }
+    return finish_reserve(c, nslots);
 }
 
 // Validate the batch so no kernel access can leave its buffers, and compute dependency levels.
@@ -703,12 +758,10 @@ extern "C" int mp2vg_batch_decode(mp2vg_ctx_t* c) {
     a.mbs = b.d_mbs;
     a.coefs = b.d_coefs;
     a.slices = b.d_slices;
-    a.pool = c->d_pool;
-    a.sink = c->d_pool + c->slot_stride * c->nslots + kSinkOff;
+    a.sink = c->d_sink + kSinkOff;
+    a.ftab = c->d_tab;
+    a.ttab = c->d_tab + c->nslots;
     a.slot_bytes = c->g.slot_bytes;
-    a.slot_stride = c->slot_stride;
-    a.tiles = c->d_tiles;
-    a.tile_stride = c->tile_stride;
     for (int i = 0; i < 3; i++) {
         a.plane_off[i] = c->g.plane_off[i];
         a.stride[i] = c->g.stride[i];
@@ -745,8 +798,8 @@ extern "C" int mp2vg_batch_decode(mp2vg_ctx_t* c) {
     for (const auto& r : b.tiles.ext_reads)
         if (r.first < c->nslots && !c->tiles_ok[r.first]) {
             const int set = std::min(r.second, nsets - 1);
-            HIPCHK(launch_tile_convert(c->d_pool + (size_t)r.first * c->slot_stride,
-                                       c->d_tiles + (size_t)r.first * c->tile_stride, c->g.cf, a, stream_of(set)));
+            HIPCHK(launch_tile_convert((const uint8_t*)(uintptr_t)c->fptr[r.first],
+                                       (uint8_t*)(uintptr_t)c->tptr[r.first], c->g.cf, a, stream_of(set)));
             c->tiles_ok[r.first] = 1;
         }
     for (const auto& w : b.tiles.writes) c->tiles_ok[w.first] = w.second;
@@ -794,8 +847,8 @@ extern "C" int mp2vg_batch_decode(mp2vg_ctx_t* c) {
             if (a.nslices) HIPCHK(launch_recon(c->g.cf, launches[i].mcm, a, st));
             for (const auto& pc : b.tiles.post)  // tiles of B pictures that later pictures read
                 if (pc.first == i)
-                    HIPCHK(launch_tile_convert(c->d_pool + (size_t)pc.second * c->slot_stride,
-                                               c->d_tiles + (size_t)pc.second * c->tile_stride, c->g.cf, a, st));
+                    HIPCHK(launch_tile_convert((const uint8_t*)(uintptr_t)c->fptr[pc.second],
+                                               (uint8_t*)(uintptr_t)c->tptr[pc.second], c->g.cf, a, st));
             if (c->launch_timing) HIPCHK(hipEventRecord(H.l[2 * i + 1], st));
             if (couple && nsets > 1) HIPCHK(hipEventRecord(c->lev[i], st));
         }
@@ -889,7 +942,7 @@ extern "C" int mp2vg_download_slot(mp2vg_ctx_t* c, int32_t slot, uint8_t* dst[3]
     HIPCHK(hipStreamSynchronize(c->stream));
     for (int p = 0; p < 3; p++) {
         size_t ds = (dst_stride && dst_stride[p]) ? (size_t)dst_stride[p] : (size_t)c->g.pw[p];
-        const uint8_t* src = c->d_pool + (size_t)slot * c->slot_stride + c->g.plane_off[p];
+        const uint8_t* src = (const uint8_t*)(uintptr_t)c->fptr[slot] + c->g.plane_off[p];
         HIPCHK(hipMemcpy2DAsync(dst[p], ds, src, c->g.stride[p], c->g.pw[p], c->g.ph[p], hipMemcpyDeviceToHost,
                                 c->stream));
     }
@@ -904,7 +957,7 @@ extern "C" int mp2vg_copy_slot_packed(mp2vg_ctx_t* c, int32_t slot, void* dst, i
     uint8_t* d = (uint8_t*)dst;
     const hipMemcpyKind kind = dst_on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
     for (int p = 0; p < 3; p++) {
-        const uint8_t* src = c->d_pool + (size_t)slot * c->slot_stride + c->g.plane_off[p];
+        const uint8_t* src = (const uint8_t*)(uintptr_t)c->fptr[slot] + c->g.plane_off[p];
         HIPCHK(hipMemcpy2DAsync(d, c->g.pw[p], src, c->g.stride[p], c->g.pw[p], c->g.ph[p], kind, c->stream));
         d += (size_t)c->g.pw[p] * c->g.ph[p];
     }
@@ -914,7 +967,7 @@ extern "C" int mp2vg_copy_slot_packed(mp2vg_ctx_t* c, int32_t slot, void* dst, i
 
 extern "C" int mp2vg_slot_device_ptr(mp2vg_ctx_t* c, int32_t slot, void** dptr) {
     if (!c || !dptr || slot < 0 || slot >= c->nslots) return MP2VG_E_INVALID;
-    *dptr = c->d_pool + (size_t)slot * c->slot_stride;
+    *dptr = (void*)(uintptr_t)c->fptr[slot];
     return MP2VG_OK;
 }
 
@@ -937,7 +990,7 @@ extern "C" int mp2vg_slot_digests(mp2vg_ctx_t* c, const int32_t* slots, int32_t 
     int32_t st[3] = {c->g.stride[0], c->g.stride[1], c->g.stride[2]};
     int32_t w[3] = {c->g.pw[0], c->g.pw[1], c->g.pw[2]};
     int32_t h[3] = {c->g.ph[0], c->g.ph[1], c->g.ph[2]};
-    HIPCHK(launch_digest(c->d_pool, c->slot_stride, c->d_dslots, n, c->g.plane_off, st, w, h, c->d_digest, c->stream));
+    HIPCHK(launch_digest(c->d_tab, c->d_dslots, n, c->g.plane_off, st, w, h, c->d_digest, c->stream));
     HIPCHK(hipMemcpyAsync(out, c->d_digest, sizeof(uint64_t) * n, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     return MP2VG_OK;
