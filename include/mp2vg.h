@@ -145,7 +145,9 @@ int  mp2vg_destroy(mp2vg_ctx_t* ctx);
 /* plane geometry of every frame slot: width/height/stride of plane 0..2, bytes per slot */
 int  mp2vg_frame_geometry(const mp2vg_config_t* cfg, int32_t width[3], int32_t height[3],
                           int32_t stride[3], uint64_t* slot_bytes);
-/* resize the frame pool (slots are uninitialised) */
+/* grow the frame pool to nslots slots (new slots read as zero).  Slots live in blocks of 16, each
+ * its own allocation, with each slot's anchor tiles (the motion-compensation taps' copy of I and
+ * P pictures, 2 x slot bytes); slot addresses are not contiguous: mp2vg_slot_device_ptr */
 int  mp2vg_reserve_slots(mp2vg_ctx_t* ctx, int32_t nslots);
 
 /* Upload a record batch from host memory (staged through pinned buffers, hipMemcpyAsync on the
@@ -192,8 +194,8 @@ int  mp2vg_copy_slot_packed(mp2vg_ctx_t* ctx, int32_t slot, void* dst, int32_t d
 /* raw device pointer of a slot (for in-HBM consumers such as a digest kernel or RCCL) */
 int  mp2vg_slot_device_ptr(mp2vg_ctx_t* ctx, int32_t slot, void** dptr);
 /* 64-bit order-independent digest of each listed slot's visible planes, computed on device:
- * sum over visible dwords d of (mix64((row << 32) | byte_x) ^ d) mod 2^64 (numpy twin:
- * tiny_mp2v_dec_amd.records.planes_digest) */
+ * sum over visible dwords d at (row, byte_x) of mix64(mix64((row << 32) | byte_x) ^ d) mod 2^64
+ * (numpy twin: tiny_mp2v_dec_amd.records.planes_digest) */
 int  mp2vg_slot_digests(mp2vg_ctx_t* ctx, const int32_t* slots, int32_t n, uint64_t* out);
 
 /* ---- stream headers ----------------------------------------------------------------------

@@ -27,7 +27,7 @@ using namespace mp2vg;
 // runtime.cpp's kernel launchers live in recon.hip (device code): never reached by validation
 namespace mp2vg {
 hipError_t launch_recon(int, int, const KArgs&, hipStream_t) { return hipErrorInvalidValue; }
-hipError_t launch_tile_convert(const uint8_t*, uint8_t*, int, const KArgs&, hipStream_t) { return hipErrorInvalidValue; }
+hipError_t launch_tile_convert(const KArgs&, int, const int32_t*, int, int32_t, hipStream_t) { return hipErrorInvalidValue; }
 hipError_t launch_digest(const uint64_t*, const int32_t*, int, const uint64_t*, const int32_t*,
                          const int32_t*, const int32_t*, unsigned long long*, hipStream_t) {
     return hipErrorInvalidValue;

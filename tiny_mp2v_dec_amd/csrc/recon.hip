@@ -1471,41 +1471,45 @@ hipError_t launch_recon(int cf, int mcm, const KArgs& a, hipStream_t stream) {
     }
 }
 
-// A slot's anchor tiles rebuilt from its frame (runtime.cpp: a batch reads a reference whose writer
-// stored no tiles -- never for an MPEG-2 stream, whose references are I/P pictures).  Thread =
-// one W-px row segment (MB column mx of row y) of one plane, stored to its two tile places.
-__global__ void __launch_bounds__(256) tile_convert_kernel(const uint8_t* __restrict__ slot, uint8_t* __restrict__ tiles,
-                                                           const Geo geo, int cw) {
-    const int plane = blockIdx.y;
-    const int w = plane == 0 ? 16 : cw;
-    const uint32_t ncol = (uint32_t)geo.stride[plane] / w, n = ncol * (uint32_t)geo.ph[plane];
-    uint8_t sink[16];
-    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
-        const uint32_t y = i / ncol, mx = i % ncol;
-        const uint8_t* src = slot + geo.plane_off[plane] + (size_t)y * geo.stride[plane] + mx * w;
-        uint8_t* tp = tiles + 2 * (size_t)geo.plane_off[plane];
-        uint32_t out[4] = {0, 0, 0, 0};
-        if (w == 16) {
-            const uint4 v = *(const uint4*)src;
-            out[0] = v.x, out[1] = v.y, out[2] = v.z, out[3] = v.w;
-            tile_store<4>(tp, mx, y, ncol, true, sink, out);
-        } else {
-            const uint2 v = *(const uint2*)src;
-            out[0] = v.x, out[1] = v.y;
-            tile_store<2>(tp, mx, y, ncol, true, sink, out);
+// Slots' anchor tiles built from their frames, in whole 128-B lines (runtime.cpp TilePlan: the B
+// pictures of a launch that later pictures read, right after it, and any reference whose writer
+// stored none).  A tile row is the frame row's bytes [W t, W t + 2 W): thread = one 16-B
+// chunk of a tile line (8 per line), read straight from the frame row.  Picture = blockIdx.y:
+// slot list[y] (or slot0 without a list).
+__global__ void __launch_bounds__(256) tile_convert_kernel(const Geo geo, int cw, const int32_t* __restrict__ list,
+                                                           int32_t slot0) {
+    const int32_t slot = list ? list[blockIdx.y] : slot0;
+    const uint8_t* frame = (const uint8_t*)geo.ftab[slot];
+    uint8_t* tiles = (uint8_t*)geo.ttab[slot];
+#pragma unroll
+    for (int plane = 0; plane < 3; plane++) {
+        const int w = plane == 0 ? 16 : cw;       // tile width class
+        const int R = w == 16 ? 4 : 8, RB = 128 / R;  // rows per tile, bytes per tile row
+        const uint32_t ncol = (uint32_t)geo.stride[plane] / w;
+        const uint32_t n = (uint32_t)geo.ph[plane] / R * ncol * 8;  // 16-B chunks of the plane
+        for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+            const uint32_t line = i >> 3, c = i & 7;
+            const uint32_t band = line / ncol, t = line % ncol;
+            const uint32_t r = c / (RB / 16), o = (c % (RB / 16)) * 16;
+            const uint8_t* src = frame + geo.plane_off[plane] + (size_t)(band * R + r) * geo.stride[plane] + t * w + o;
+            const uint2 lo = *(const uint2*)src, hi = *(const uint2*)(src + 8);
+            *(uint4*)(tiles + 2 * (size_t)geo.plane_off[plane] + (size_t)line * 128 + c * 16) =
+                make_uint4(lo.x, lo.y, hi.x, hi.y);
         }
     }
 }
 
-hipError_t launch_tile_convert(const uint8_t* slot, uint8_t* tiles, int cf, const KArgs& a, hipStream_t stream) {
+hipError_t launch_tile_convert(const KArgs& a, int cf, const int32_t* d_list, int n, int32_t slot0, hipStream_t stream) {
     Geo g;
+    g.ftab = a.ftab;
+    g.ttab = a.ttab;
     for (int i = 0; i < 3; i++) {
         g.plane_off[i] = (uint32_t)a.plane_off[i];
         g.stride[i] = a.stride[i];
         g.ph[i] = a.ph[i];
     }
     const int cw = cf == 3 ? 16 : 8;  // chroma MB width
-    hipLaunchKernelGGL(tile_convert_kernel, dim3(256, 3), dim3(256), 0, stream, slot, tiles, g, cw);
+    hipLaunchKernelGGL(tile_convert_kernel, dim3(128, d_list ? n : 1), dim3(256), 0, stream, g, cw, d_list, slot0);
     return hipGetLastError();
 }
 
