@@ -510,46 +510,17 @@ __device__ __forceinline__ void issue_pass(const LaneRec& L, bool live, int lane
                                    (fl >> (9 + 2 * r)) & 1, stride, ph);
 }
 
-// The frame_c rows: no kernel reads them back (the taps read the anchor tiles), so they can be
-// stored nontemporally (MP2VG_NT_ROWS: dev A/B) and leave L2 to the tiles and the references
-#ifndef MP2VG_NT_ROWS
-#define MP2VG_NT_ROWS 0
-#endif
-typedef uint32_t u2v __attribute__((ext_vector_type(2)));
+// frame_c row stores (16 / 8 B).  Nontemporal stores measured c2 -8.5 %, c3 -19 % (round 4).
 __device__ __forceinline__ void row_store16(uint8_t* d, uint32_t a, uint32_t b, uint32_t c, uint32_t e) {
-    if (MP2VG_NT_ROWS)
-        __builtin_nontemporal_store(u4v{a, b, c, e}, (u4v*)d);
-    else
-        *(uint4*)d = make_uint4(a, b, c, e);
+    *(uint4*)d = make_uint4(a, b, c, e);
 }
-__device__ __forceinline__ void row_store8(uint8_t* d, uint32_t a, uint32_t b) {
-    if (MP2VG_NT_ROWS)
-        __builtin_nontemporal_store(u2v{a, b}, (u2v*)d);
-    else
-        *(uint2*)d = make_uint2(a, b);
-}
+__device__ __forceinline__ void row_store8(uint8_t* d, uint32_t a, uint32_t b) { *(uint2*)d = make_uint2(a, b); }
 
 // ---- add/clip + store ----------------------------------------------------------------------
-// An anchor row's two tile copies (tile_off): its own tile and the apron of the tile to its left
-// (MB column 0 has none).  Dead lanes write the wave's sink line.
-template <int NW>
-__device__ __forceinline__ void tile_store(uint8_t* tplane, uint32_t mx, uint32_t y, uint32_t ncol, bool live,
-                                           uint8_t* wsink, const uint32_t (&out)[4]) {
-    constexpr int W = 4 * NW;
-    const uint32_t o = tile_row<W>(mx, y, ncol);
-    uint8_t* d0 = live ? tplane + o : wsink;
-    uint8_t* d1 = (live && mx) ? tplane + (o - 128u + W) : wsink;
-    if (NW == 4) {
-        *(uint4*)d0 = make_uint4(out[0], out[1], out[2], out[3]);
-        *(uint4*)d1 = make_uint4(out[0], out[1], out[2], out[3]);
-    } else {
-        *(uint2*)d0 = make_uint2(out[0], out[1]);
-        *(uint2*)d1 = make_uint2(out[0], out[1]);
-    }
-}
 
-// tiles (uniform: the picture is read by a later one, runtime.cpp TilePlan): the row also goes
-// to the picture's anchor tiles (tile_store)
+// tiles (uniform: the picture is read by a later one, runtime.cpp TilePlan): the row's pixels
+// also go over the first half of its int16 residual row in LDS, from which tile_group writes the
+// picture's anchor tiles in whole lines
 template <int CF, int J, int NW, int ABL>
 __device__ __forceinline__ void store_pass(uint32_t r0, uint32_t r1, bool live, int lane, const Geo& geo, uint8_t* wsink,
                                            uint8_t* dst_slot, uint8_t* dst_tiles, bool tiles, const short* s_res_wave,
@@ -640,14 +611,16 @@ __device__ __forceinline__ void store_pass_put8(uint32_t r0, bool live, int lane
     }
 }
 
-// I kernels: the group's anchor tiles written from the byte residual image in whole tile lines.
+// The group's anchor tiles, written in whole tile lines from LDS (I kernels: the byte residual
+// image; P loops: the pixels store_pass left in the residual image).
 // A group of 4 MBs (columns t0..t0+3) owns tiles t0..t0+2 of each band completely and two half
 // tiles: t0+3's own half (MB 3) and t0-1's apron half (MB 0; none at column 0).  Unit u of a
 // W-16 plane: u < 96 -> tile t0 + (u >> 5), band (u >> 3) & 3 of the MB row, chunk u & 7 (row
 // chunk >> 1, half chunk & 1: MB j + half), so 8 consecutive lanes fill one 128-B line; 96..127 ->
 // the half tiles' 16-B rows.  A W-8 plane (4:2:0 / 4:2:2 chroma): 16-B units are whole tile rows
 // [MB j row | MB j+1 row] of tiles t0..t0+2, 8-B units the half tiles' rows.  Row stores of the
-// same bytes (tile_store, one row per lane) left 16-B pieces 32 B apart in every line.
+// same bytes (one row per lane, own and apron place) left 16-B pieces 32 B apart in every line:
+// I launch +35-60 % instead of +30 % (profiles/r4/README.md).
 // a row of the group's pixels from LDS: the I kernels' byte residual image (compact layout, each
 // dword in the x0, x0+2, x0+1, x0+3 order of ResLayout: one v_perm); P/B kernels (NAT): the
 // final pixels in natural order that store_pass left in the first half of each int16 residual row

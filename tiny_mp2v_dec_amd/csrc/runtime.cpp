@@ -338,24 +338,14 @@ extern "C" int mp2vg_reserve_slots(mp2vg_ctx_t* c, int32_t nslots) {
         (void)hipGetLastError();
         p = nullptr;
     }
-    // 2 = the pool and tiles allocated while a same-size block is held (freed after), 3 = after
-    // such a block was allocated and freed: is the placement of a process's first big allocation
-    // the slow one (profiles/r4/README.md)?
-    uint8_t* dummy = nullptr;
-    if (pool_alloc == 2 || pool_alloc == 3) {
-        if (hipMalloc((void**)&dummy, bytes + tbytes) != hipSuccess) (void)hipGetLastError(), dummy = nullptr;
-        if (dummy && pool_alloc == 3) hipFree(dummy), dummy = nullptr;
-    }
-    if (pool_alloc == 4 && hipMalloc((void**)&t, tbytes) != hipSuccess) (void)hipGetLastError(), t = nullptr;  // tiles first
     static uint8_t* ballast = nullptr;  // 5: the process's first block (pool-sized, or MP2VG_BALLAST_MB) is held for good
     static const size_t ballast_mb = getenv("MP2VG_BALLAST_MB") ? (size_t)atoll(getenv("MP2VG_BALLAST_MB")) : 0;
     if (pool_alloc == 5 && !ballast &&
         hipMalloc((void**)&ballast, ballast_mb ? ballast_mb << 20 : bytes + tbytes) != hipSuccess)
         (void)hipGetLastError(), ballast = nullptr;
     if (!p) HIPCHK(hipMalloc((void**)&p, bytes));
-    if (!t && hipMalloc((void**)&t, tbytes) != hipSuccess) {
+    if (hipMalloc((void**)&t, tbytes) != hipSuccess) {
         hipFree(p);
-        if (dummy) hipFree(dummy);
         set_error("out of device memory for the anchor tiles");
         return MP2VG_E_HIP;
     }
@@ -369,7 +359,6 @@ extern "C" int mp2vg_reserve_slots(mp2vg_ctx_t* c, int32_t nslots) {
         HIPCHK(hipFree(c->d_tiles));
     }
     HIPCHK(hipStreamSynchronize(c->stream));
-    if (dummy) hipFree(dummy);
     c->d_pool = p;
     c->d_tiles = t;
     c->fptr.resize(nslots);
