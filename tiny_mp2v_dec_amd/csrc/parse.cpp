@@ -412,14 +412,24 @@ void parse_slice(const Ctx& C, const PicWork& P, const SliceJob& job, mp2vg_mb_t
                     i = 1;
                 }
             }
-            // parse_block's VLC loop (mb_decoder.cpp:89-149): one refill per code
+            // parse_block's VLC loop (mb_decoder.cpp:89-149): one refill per two codes (a refill
+            // leaves >= 56 bits; a code takes at most 24, an escape)
             for (;;) {
                 int run, level;
                 r.refill();
-                const int kind = CoefLut::decode_tab(lut1, lut2, r, run, level);
+                int kind = CoefLut::decode_tab(lut1, lut2, r, run, level);
                 if (kind != CoefLut::NORMAL) {  // escapes come back as NORMAL (:100-104)
                     if (kind < 0) FAIL(MP2VG_E_BITSTREAM, "bad DCT coefficient code");
                     break;  // EOB
+                }
+                i += run;
+                if (__builtin_expect(i > 63, 0)) FAIL(MP2VG_E_BITSTREAM, "coefficient run past position 63");
+                *w++ = ((uint32_t)level & 0xffffu) | ((uint32_t)i << 16) | btag;
+                i++;
+                kind = CoefLut::decode_tab(lut1, lut2, r, run, level);
+                if (kind != CoefLut::NORMAL) {
+                    if (kind < 0) FAIL(MP2VG_E_BITSTREAM, "bad DCT coefficient code");
+                    break;
                 }
                 i += run;
                 if (__builtin_expect(i > 63, 0)) FAIL(MP2VG_E_BITSTREAM, "coefficient run past position 63");
