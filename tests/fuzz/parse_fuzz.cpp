@@ -35,13 +35,19 @@ hipError_t launch_digest(const uint64_t*, const int32_t*, int, const uint64_t*, 
 }  // namespace mp2vg
 static long g_valid = 0, g_invalid = 0;
 
+// must_pass: the records are the parser's own output, which the drop-in uploads without this
+// check (trusted path): the parser must uphold every invariant the validation enforces
 static void validate(const mp2vg_config_t& cfg, std::vector<mp2vg_picture_t>& pics, std::vector<mp2vg_mb_t>& mbs,
-                     std::vector<uint32_t>& coefs, int32_t nslots) {
+                     std::vector<uint32_t>& coefs, int32_t nslots, bool must_pass = false) {
     int32_t nl = 0;
     std::vector<int32_t> lop(pics.size() + 1), mode(64);
     const int rc = mp2vg_batch_validate(&cfg, nslots, pics.data(), (int32_t)pics.size(), mbs.data(), mbs.size(),
                                         coefs.data(), coefs.size(), &nl, lop.data(), mode.data(), 64);
     (rc == MP2VG_OK ? g_valid : g_invalid)++;
+    if (must_pass && rc != MP2VG_OK) {
+        fprintf(stderr, "parser output rejected by the upload validation: %s\n", mp2vg_last_error());
+        abort();
+    }
 }
 
 static void corrupt_and_validate(const mp2vg_config_t& cfg, const mp2vg_parsed_t* p, std::mt19937_64& rng) {
@@ -52,7 +58,7 @@ static void corrupt_and_validate(const mp2vg_config_t& cfg, const mp2vg_parsed_t
     std::vector<mp2vg_picture_t> pics(mp2vg_parsed_pictures(p), mp2vg_parsed_pictures(p) + n);
     std::vector<mp2vg_mb_t> mbs(mp2vg_parsed_mbs(p), mp2vg_parsed_mbs(p) + nm);
     std::vector<uint32_t> coefs(mp2vg_parsed_coefs(p), mp2vg_parsed_coefs(p) + nc);
-    validate(cfg, pics, mbs, coefs, n);
+    validate(cfg, pics, mbs, coefs, n, true);
     const int k = 1 + (int)(rng() % 4);
     for (int i = 0; i < k; i++) {
         const int what = (int)(rng() % 10);

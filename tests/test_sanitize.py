@@ -7,7 +7,10 @@ mp2vg_batch_validate, no device needed).  Over the golden streams it feeds bit f
 spans, truncations, deleted / duplicated spans and injected start codes to the whole-stream
 parse and to the drop-in's streaming parse session, and records with corrupted fields to the
 validation.  Rejections are expected; any out-of-bounds access, leak or undefined behaviour
-aborts the harness (-fno-sanitize-recover=all) and fails the test.  Findings so far, fixed:
+aborts the harness (-fno-sanitize-recover=all) and fails the test.  The records of every mutant
+that parses must pass the full upload validation unmodified: the drop-in uploads the parser's
+records on the trusted path, so the parser itself has to uphold every invariant the kernels rely
+on.  Findings so far, fixed:
 a zero-picture stream passed a null pointer to memcpy, and f_code = 0 made the motion-vector
 parse read -1 bits (now rejected like the reference's undefined read)."""
 import json
