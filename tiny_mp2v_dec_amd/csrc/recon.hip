@@ -217,9 +217,18 @@ __device__ __forceinline__ T gsel(const T (&v)[3], int plane) {
 // 32-63 repeat 0-31).  Per-lane fields of a lane's own MB come out with one ds_bpermute,
 // wave-uniform fields with v_readlane.  Loading it is one coalesced global_load_dword, issued
 // two groups ahead.
+// MP2VG_REC_NT (round 5 A/B): records and coefficient words, read once by one CU, loaded
+// nontemporal (streaming) so that they do not displace reference tiles from L2
+#ifndef MP2VG_REC_NT
+#define MP2VG_REC_NT 0
+#endif
+__device__ __forceinline__ uint32_t ld_rec(const uint32_t* p) {
+    if (MP2VG_REC_NT) return __builtin_nontemporal_load(p);
+    return *p;
+}
 __device__ __forceinline__ uint32_t rec_load(const uint32_t* __restrict__ mbrec, uint32_t g, uint32_t mb_last, int lane) {
     const uint32_t mb = min(g + (uint32_t)(lane & 3), mb_last);
-    return mbrec[(size_t)mb * 8 + ((lane >> 2) & 7)];
+    return ld_rec(&mbrec[(size_t)mb * 8 + ((lane >> 2) & 7)]);
 }
 __device__ __forceinline__ uint32_t rec_get(uint32_t rv, int f, int k) {  // lane-varying f, k
     return (uint32_t)__builtin_amdgcn_ds_bpermute((f * 4 + k) * 4, (int)rv);
@@ -516,6 +525,32 @@ __device__ __forceinline__ void row_store16(uint8_t* d, uint32_t a, uint32_t b, 
 }
 __device__ __forceinline__ void row_store8(uint8_t* d, uint32_t a, uint32_t b) { *(uint2*)d = make_uint2(a, b); }
 
+// Cache policy of the frame-row and anchor-tile stores: 0 = plain global stores; otherwise
+// buffer stores through the slot's resource with these aux bits (gfx950: 1 sc0, 2 nt, 16 sc1),
+// dead lanes at an out-of-range offset (the store is discarded).  Measured, c2, two boxes, same-box
+// arms interleaved (profiles/r5/README.md):
+//   tiles nt (streaming: the lines stay in L2 but go first)  +4.0-4.8 %  (the I launch -10-13 %)
+//   tiles sc1 (write through, line dropped from L2)           -0.2 %
+//   tiles nt + sc1                                            +1.6 %
+//   rows sc1 (no kernel reads the frame_c rows back)          +1.5 % alone, +0.5 % over tiles nt
+//   rows nt                                                   -3.5 % over tiles nt
+//   records + coefficient words nt loads                      -0.5 %
+#ifndef MP2VG_ROW_POL
+#define MP2VG_ROW_POL 16
+#endif
+#ifndef MP2VG_TILE_POL
+#define MP2VG_TILE_POL 2
+#endif
+template <int POL>
+__device__ __forceinline__ void pol_store16(__amdgpu_buffer_rsrc_t r, uint32_t off, uint4 v) {
+    __builtin_amdgcn_raw_buffer_store_b128(u4v{v.x, v.y, v.z, v.w}, r, (int)off, 0, POL);
+}
+template <int POL>
+__device__ __forceinline__ void pol_store8(__amdgpu_buffer_rsrc_t r, uint32_t off, uint2 v) {
+    typedef uint32_t u2v __attribute__((ext_vector_type(2)));
+    __builtin_amdgcn_raw_buffer_store_b64(u2v{v.x, v.y}, r, (int)off, 0, POL);
+}
+
 // ---- add/clip + store ----------------------------------------------------------------------
 
 // tiles (uniform: the picture is read by a later one, runtime.cpp TilePlan): the row's pixels
@@ -523,8 +558,8 @@ __device__ __forceinline__ void row_store8(uint8_t* d, uint32_t a, uint32_t b) {
 // picture's anchor tiles in whole lines
 template <int CF, int J, int NW, int ABL>
 __device__ __forceinline__ void store_pass(uint32_t r0, uint32_t r1, bool live, int lane, const Geo& geo, uint8_t* wsink,
-                                           uint8_t* dst_slot, uint8_t* dst_tiles, bool tiles, const short* s_res_wave,
-                                           const uint32_t (&p)[NW]) {
+                                           uint8_t* dst_slot, __amdgpu_buffer_rsrc_t dst_rsrc, bool tiles,
+                                           const short* s_res_wave, const uint32_t (&p)[NW]) {
     using F = Fmt<CF>;
     using RL = ResLayout<CF>;
     int k, plane, py;
@@ -561,8 +596,9 @@ __device__ __forceinline__ void store_pass(uint32_t r0, uint32_t r1, bool live, 
     }
     const int pw = plane == 0 ? 16 : F::CW;
     const int phm = plane == 0 ? 16 : F::CH;
-    uint8_t* dst = dst_slot + gsel(geo.plane_off, plane) +
-                   mul24_asm((r0 >> 16) * phm + py, (uint32_t)gsel(geo.stride, plane)) + (int)(r0 & 0xffff) * pw;
+    const uint32_t doff = gsel(geo.plane_off, plane) + mul24_asm((r0 >> 16) * phm + py, (uint32_t)gsel(geo.stride, plane)) +
+                          (r0 & 0xffff) * (uint32_t)pw;
+    uint8_t* dst = dst_slot + doff;
     dst = live ? dst : wsink;  // branch-free: every lane stores (see Tap)
     if (ABL & 8192)  // dev ablation (timing only): each store instruction writes 1 KB contiguous
         dst = dst_slot + ((((r0 & 0xffff) + (r0 >> 16) * 128u) * 3u + (uint32_t)J) * 1024u + (uint32_t)lane * 16u) %
@@ -579,6 +615,11 @@ __device__ __forceinline__ void store_pass(uint32_t r0, uint32_t r1, bool live, 
     } else if (ABL & 4096) {  // dev ablation (timing only): one dword per row store (1/4, 1/2 bytes)
         asm volatile("" ::"v"(out[0]), "v"(out[1]), "v"(out[2]), "v"(out[3]));
         *(uint32_t*)dst = out[0] ^ out[1] ^ (NW == 4 ? out[2] ^ out[3] : 0u);
+    } else if (MP2VG_ROW_POL != 0) {
+        if (NW == 4)
+            pol_store16<MP2VG_ROW_POL>(dst_rsrc, live ? doff : kNoTap, make_uint4(out[0], out[1], out[2], out[3]));
+        else
+            pol_store8<MP2VG_ROW_POL>(dst_rsrc, live ? doff : kNoTap, make_uint2(out[0], out[1]));
     } else if (NW == 4) {
         row_store16(dst, out[0], out[1], out[2], out[3]);
     } else {
@@ -590,7 +631,8 @@ __device__ __forceinline__ void store_pass(uint32_t r0, uint32_t r1, bool live, 
 // ResLayout order (x0, x0+2, x0+1, x0+3 in each 4-pixel group) by one v_perm per dword
 template <int CF, int J, int NW>
 __device__ __forceinline__ void store_pass_put8(uint32_t r0, bool live, int lane, const Geo& geo, uint8_t* wsink,
-                                                uint8_t* dst_slot, const uint8_t* res8_wave) {
+                                                uint8_t* dst_slot, __amdgpu_buffer_rsrc_t dst_rsrc,
+                                                const uint8_t* res8_wave) {
     using F = Fmt<CF>;
     using RL = ResLayout<CF>;
     int k, plane, py;
@@ -598,16 +640,24 @@ __device__ __forceinline__ void store_pass_put8(uint32_t r0, bool live, int lane
     const uint8_t* row = &res8_wave[k * RL::SIZE + RL::base(plane) + py * RL::width(plane)];
     const int pw = plane == 0 ? 16 : F::CW;
     const int phm = plane == 0 ? 16 : F::CH;
-    uint8_t* dst = dst_slot + gsel(geo.plane_off, plane) +
-                   mul24_asm((r0 >> 16) * phm + py, (uint32_t)gsel(geo.stride, plane)) + (int)(r0 & 0xffff) * pw;
-    dst = live ? dst : wsink;  // branch-free: every lane stores (see Tap)
+    const uint32_t doff = gsel(geo.plane_off, plane) + mul24_asm((r0 >> 16) * phm + py, (uint32_t)gsel(geo.stride, plane)) +
+                          (r0 & 0xffff) * (uint32_t)pw;
+    uint8_t* dst = live ? dst_slot + doff : wsink;  // branch-free: every lane stores (see Tap)
     if (NW == 4) {
         const uint4 q = *(const uint4*)row;
-        row_store16(dst, __builtin_amdgcn_perm(q.x, q.x, 0x03010200u), __builtin_amdgcn_perm(q.y, q.y, 0x03010200u),
-                                  __builtin_amdgcn_perm(q.z, q.z, 0x03010200u), __builtin_amdgcn_perm(q.w, q.w, 0x03010200u));
+        const uint4 o = make_uint4(__builtin_amdgcn_perm(q.x, q.x, 0x03010200u), __builtin_amdgcn_perm(q.y, q.y, 0x03010200u),
+                                   __builtin_amdgcn_perm(q.z, q.z, 0x03010200u), __builtin_amdgcn_perm(q.w, q.w, 0x03010200u));
+        if (MP2VG_ROW_POL != 0)
+            pol_store16<MP2VG_ROW_POL>(dst_rsrc, live ? doff : kNoTap, o);
+        else
+            row_store16(dst, o.x, o.y, o.z, o.w);
     } else {
         const uint2 q = *(const uint2*)row;
-        row_store8(dst, __builtin_amdgcn_perm(q.x, q.x, 0x03010200u), __builtin_amdgcn_perm(q.y, q.y, 0x03010200u));
+        const uint2 o = make_uint2(__builtin_amdgcn_perm(q.x, q.x, 0x03010200u), __builtin_amdgcn_perm(q.y, q.y, 0x03010200u));
+        if (MP2VG_ROW_POL != 0)
+            pol_store8<MP2VG_ROW_POL>(dst_rsrc, live ? doff : kNoTap, o);
+        else
+            row_store8(dst, o.x, o.y);
     }
 }
 
@@ -642,8 +692,9 @@ __device__ __forceinline__ uint2 img_row8(const uint8_t* img, int k, int plane, 
 }
 template <int CF, bool NAT, int ABL = 0>
 __device__ __forceinline__ void tile_group(uint32_t mx0, uint32_t mby, int lane, const Geo& geo, uint8_t* wsink,
-                                           uint8_t* dst_tiles, const uint8_t* res8) {
+                                           uint8_t* dst_tiles, __amdgpu_buffer_rsrc_t tile_rsrc, const uint8_t* res8) {
     using F = Fmt<CF>;
+    constexpr bool POL = MP2VG_TILE_POL != 0;
     // W-16 planes: luma, and the 4:4:4 chroma planes
     for (int plane = 0; plane < (CF == 3 && kChromaTiles ? 3 : 1); plane++) {
         uint8_t* tp = dst_tiles + 2u * gsel(geo.plane_off, plane);
@@ -661,7 +712,10 @@ __device__ __forceinline__ void tile_group(uint32_t mx0, uint32_t mby, int lane,
             const uint4 v = img_row16<CF, NAT>(res8, j + h, plane, r);
             const bool none = j < 0 && mx0 == 0;
             const uint32_t o = tile_row<16>(mx0 + (uint32_t)j, mby * 16u + (uint32_t)r, ncol) + (uint32_t)h * 16u;
-            *(uint4*)(none ? wsink : ((ABL & 65536) ? dst_tiles + (o & 0xFFF0u) : tp + o)) = v;
+            if (POL)
+                pol_store16<MP2VG_TILE_POL>(tile_rsrc, none ? kNoTap : 2u * gsel(geo.plane_off, plane) + o, v);
+            else
+                *(uint4*)(none ? wsink : ((ABL & 65536) ? dst_tiles + (o & 0xFFF0u) : tp + o)) = v;
         }
     }
     if constexpr (CF != 3 && kChromaTiles) {  // W-8 chroma: Cb and Cr
@@ -675,8 +729,13 @@ __device__ __forceinline__ void tile_group(uint32_t mx0, uint32_t mby, int lane,
             const int j = rem / RPM, r = rem % RPM;
             const uint2 a = img_row8<CF, NAT>(res8, j, plane, r), b = img_row8<CF, NAT>(res8, min(j + 1, 3), plane, r);
             const uint32_t o = tile_row<8>(mx0 + (uint32_t)j, mby * (uint32_t)RPM + (uint32_t)r, ncol);
-            uint8_t* d = (ABL & 65536) ? dst_tiles + (o & 0xFFF0u) : dst_tiles + 2u * gsel(geo.plane_off, plane) + o;
-            *(uint4*)(u < N16 ? d : wsink) = make_uint4(a.x, a.y, b.x, b.y);
+            if (POL) {
+                pol_store16<MP2VG_TILE_POL>(tile_rsrc, u < N16 ? 2u * gsel(geo.plane_off, plane) + o : kNoTap,
+                                            make_uint4(a.x, a.y, b.x, b.y));
+            } else {
+                uint8_t* d = (ABL & 65536) ? dst_tiles + (o & 0xFFF0u) : dst_tiles + 2u * gsel(geo.plane_off, plane) + o;
+                *(uint4*)(u < N16 ? d : wsink) = make_uint4(a.x, a.y, b.x, b.y);
+            }
         }
 #pragma nounroll
         for (int i = 0; i < (N8 + 63) / 64; i++) {
@@ -687,8 +746,12 @@ __device__ __forceinline__ void tile_group(uint32_t mx0, uint32_t mby, int lane,
             const uint2 v = img_row8<CF, NAT>(res8, side ? 0 : 3, plane, r);
             const uint32_t o = tile_row<8>(mx0 + (uint32_t)j, mby * (uint32_t)RPM + (uint32_t)r, ncol) + (uint32_t)h * 8u;
             const bool none = u >= N8 || (side && mx0 == 0);
-            uint8_t* d = (ABL & 65536) ? dst_tiles + (o & 0xFFF8u) : dst_tiles + 2u * gsel(geo.plane_off, plane) + o;
-            *(uint2*)(none ? wsink : d) = v;
+            if (POL) {
+                pol_store8<MP2VG_TILE_POL>(tile_rsrc, none ? kNoTap : 2u * gsel(geo.plane_off, plane) + o, v);
+            } else {
+                uint8_t* d = (ABL & 65536) ? dst_tiles + (o & 0xFFF8u) : dst_tiles + 2u * gsel(geo.plane_off, plane) + o;
+                *(uint2*)(none ? wsink : d) = v;
+            }
         }
     }
 }
@@ -792,6 +855,7 @@ struct SliceCtx {
     const uint32_t* coefs;
     uint8_t* dst_slot;
     uint8_t* dst_tiles;  // the picture's anchor tiles
+    __amdgpu_buffer_rsrc_t dst_rsrc, tile_rsrc;  // the same as buffer resources (store policies)
     bool tiles;          // ... which it writes (SliceDesc.reserved bit 0, runtime.cpp TilePlan)
     // this wave's own 64-B sink line (dummy and dead-lane stores): stores of many waves to one
     // address serialize in one L2 channel, and a wave's first loop-head wait covers its own
@@ -929,13 +993,13 @@ __device__ __forceinline__ void prefetch_words(uint32_t (&cw)[NCW], const SliceC
                                                int lane) {
     if (MCM != 0) {
 #pragma unroll
-        for (int j = 0; j < NCW; j++) cw[j] = c.coefs[coef0 + 64 * j + lane];
+        for (int j = 0; j < NCW; j++) cw[j] = ld_rec(&c.coefs[coef0 + 64 * j + lane]);
     } else {
         const uint32_t off = (coef0 + (uint32_t)lane) * 4u;
 #pragma unroll
         for (int j = 0; j < NCW; j++)
             cw[j] = __builtin_amdgcn_raw_buffer_load_b32(c.coef_rsrc, 64 * j < ncoef ? (int)(off + 256u * j) : (int)kNoTap,
-                                                         0, 0);
+                                                         0, MP2VG_REC_NT ? 2 : 0);
     }
 }
 
@@ -1060,7 +1124,7 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, LT&
 #pragma unroll
                     for (int j = 0; j < XW; j++) {
                         const int wi = base + 64 * j + lane;
-                        xw[j] = wi < S.ncoef ? c.coefs[S.coef0 + wi] : 0u;
+                        xw[j] = wi < S.ncoef ? ld_rec(&c.coefs[S.coef0 + wi]) : 0u;
                     }
 #pragma unroll
                     for (int j = 0; j < XW; j++)
@@ -1228,21 +1292,22 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, LT&
         // ---- E. prediction + residual, one row store per lane ----
         if constexpr (LT::COMPACT) {
             const uint8_t* res8 = (const uint8_t*)L.res[wave];
-            store_pass_put8<CF, 0, 4>(gr0, glive, lane, geo, c.wsink, c.dst_slot, res8);
-            store_pass_put8<CF, 1, NWC>(gr0, glive, lane, geo, c.wsink, c.dst_slot, res8);
-            if (CF != 1) store_pass_put8<CF, 2, NWC>(gr0, glive, lane, geo, c.wsink, c.dst_slot, res8);
+            store_pass_put8<CF, 0, 4>(gr0, glive, lane, geo, c.wsink, c.dst_slot, c.dst_rsrc, res8);
+            store_pass_put8<CF, 1, NWC>(gr0, glive, lane, geo, c.wsink, c.dst_slot, c.dst_rsrc, res8);
+            if (CF != 1) store_pass_put8<CF, 2, NWC>(gr0, glive, lane, geo, c.wsink, c.dst_slot, c.dst_rsrc, res8);
             if (c.tiles) {  // MB 0 of the group is always live
                 const uint32_t r00 = (uint32_t)__builtin_amdgcn_readfirstlane((int)gr0);
-                tile_group<CF, false, ABL>(r00 & 0xffff, r00 >> 16, lane, geo, c.wsink, c.dst_tiles, res8);
+                tile_group<CF, false, ABL>(r00 & 0xffff, r00 >> 16, lane, geo, c.wsink, c.dst_tiles, c.tile_rsrc, res8);
             }
         } else {
-            store_pass<CF, 0, 4, ABL>(gr0, gr1, glive, lane, geo, c.wsink, c.dst_slot, c.dst_tiles, MCM != 2 && c.tiles, L.res[wave], p0);
-            store_pass<CF, 1, NWC, ABL>(gr0, gr1, glive, lane, geo, c.wsink, c.dst_slot, c.dst_tiles, MCM != 2 && c.tiles, L.res[wave], p1);
-            if (CF != 1) store_pass<CF, 2, NWC, ABL>(gr0, gr1, glive, lane, geo, c.wsink, c.dst_slot, c.dst_tiles, MCM != 2 && c.tiles, L.res[wave], p2);
+            store_pass<CF, 0, 4, ABL>(gr0, gr1, glive, lane, geo, c.wsink, c.dst_slot, c.dst_rsrc, MCM != 2 && c.tiles, L.res[wave], p0);
+            store_pass<CF, 1, NWC, ABL>(gr0, gr1, glive, lane, geo, c.wsink, c.dst_slot, c.dst_rsrc, MCM != 2 && c.tiles, L.res[wave], p1);
+            if (CF != 1) store_pass<CF, 2, NWC, ABL>(gr0, gr1, glive, lane, geo, c.wsink, c.dst_slot, c.dst_rsrc, MCM != 2 && c.tiles, L.res[wave], p2);
             if (MCM != 2 && c.tiles) {  // the pixels store_pass left in the residual image, as whole tile lines
                 wave_sync();
                 const uint32_t r00 = (uint32_t)__builtin_amdgcn_readfirstlane((int)gr0);
-                tile_group<CF, true, ABL>(r00 & 0xffff, r00 >> 16, lane, geo, c.wsink, c.dst_tiles, (const uint8_t*)L.res[wave]);
+                tile_group<CF, true, ABL>(r00 & 0xffff, r00 >> 16, lane, geo, c.wsink, c.dst_tiles, c.tile_rsrc,
+                                          (const uint8_t*)L.res[wave]);
             }
         }
         wave_sync();
@@ -1307,6 +1372,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MCM == 0 &&
     c.dst_slot = (uint8_t*)geo.ftab[pic->dst_slot];
     c.wsink = geo.sink + 2048 + ((b * WAVES + wave) & 1023) * 64;
     c.dst_tiles = (uint8_t*)geo.ttab[pic->dst_slot];
+    c.dst_rsrc = slot_rsrc(c.dst_slot, (uint32_t)geo.slot_bytes);
+    c.tile_rsrc = slot_rsrc(c.dst_tiles, (uint32_t)(2 * geo.slot_bytes));
     c.tiles = sd.reserved & 1u;
     // the taps read the references' anchor tiles (tile slot = 2 x slot bytes)
     const int fs = pic->fwd_slot < 0 ? pic->dst_slot : pic->fwd_slot;
