@@ -120,6 +120,11 @@ def per_picture_bytes(parsed):
     return frame + mb_bytes * dirs.sum(1) + 32 * n + 4 * ncoef.sum(1)
 
 
+# records.planes_digest's formula (2: mix64(mix64((row << 32) | x) ^ d), round 4); the golden
+# digest file records the format its entries were computed with
+DIGEST_FORMAT = 2
+
+
 def expected_digests(config, gops, seed):
     """Per-slot (decode order) frame digests of this bench workload from the compiled reference
     (tests/golden/bench_digests.npz, written by tests/golden/make_bench_digests.py), or None."""
@@ -127,6 +132,10 @@ def expected_digests(config, gops, seed):
     if not os.path.exists(path):
         return None
     with np.load(path) as d:
+        fmt = int(d["digest_format"][0]) if "digest_format" in d.files else 1
+        if fmt != DIGEST_FORMAT:
+            raise SystemExit(f"{path}: digest format {fmt}, this build computes format {DIGEST_FORMAT} "
+                             "(tests/golden/make_bench_digests.py)")
         key = f"{config}_g{gops}_s{seed}"
         return d[key].copy() if key in d else None
 

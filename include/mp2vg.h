@@ -191,8 +191,17 @@ int  mp2vg_download_slot(mp2vg_ctx_t* ctx, int32_t slot, uint8_t* dst_planes[3],
  * layout, tiny_mp2v_dec.cpp:11-17) to dst: HBM of the context's device when dst_on_device
  * (e.g. an RCCL send buffer for the rank-0 frame gather), else host memory; synchronous */
 int  mp2vg_copy_slot_packed(mp2vg_ctx_t* ctx, int32_t slot, void* dst, int32_t dst_on_device);
-/* raw device pointer of a slot (for in-HBM consumers such as a digest kernel or RCCL) */
+/* raw device pointer of a slot (for in-HBM consumers such as a digest kernel or RCCL).  The
+ * slot is READ-ONLY for callers: the motion-compensation taps read a reference from its anchor
+ * tiles, a second copy the decode writes next to the frame (recon.hip), so bytes written through
+ * this pointer are not seen by later predictions unless the caller then calls
+ * mp2vg_invalidate_slot, which makes the next decode that reads the slot rebuild its tiles. */
 int  mp2vg_slot_device_ptr(mp2vg_ctx_t* ctx, int32_t slot, void** dptr);
+/* the slot's frame was written by someone other than the decode (an RCCL receive, an external
+ * producer writing through mp2vg_slot_device_ptr): its anchor tiles are stale.  The next batch
+ * that predicts from the slot rebuilds them from the frame first (tile_convert).  Call it after
+ * the writes have completed and before mp2vg_batch_decode of a batch that reads the slot. */
+int  mp2vg_invalidate_slot(mp2vg_ctx_t* ctx, int32_t slot);
 /* 64-bit order-independent digest of each listed slot's visible planes, computed on device:
  * sum over visible dwords d at (row, byte_x) of mix64(mix64((row << 32) | byte_x) ^ d) mod 2^64
  * (numpy twin: tiny_mp2v_dec_amd.records.planes_digest) */

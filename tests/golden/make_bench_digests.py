@@ -7,6 +7,7 @@ written exactly as bench.py writes it, decoded by the compiled reference at num_
 each frame's digest (records.planes_digest, computed in ref_decode's render callback) is stored
 in decode order, the order of bench.py's slots:
   tests/golden/bench_digests.npz   key "<config>_g<gops>_s<seed>" -> uint64[frames]
+                                   key "digest_format" -> [DIGEST_FORMAT]
 bench.py compares its device digests with these after the timed region and reports
 "parity": "bit-exact" (or fails).  The reference's scheduler can render a stale pool slot
 (see make_stream_fixtures.py), which shows as a repeated frame digest: such runs are retried.
@@ -27,6 +28,10 @@ import bench  # noqa: E402
 from tiny_mp2v_dec_amd import records as R  # noqa: E402
 
 RANKS = 8
+# the digest formula the entries were computed with (records.planes_digest): 1 = round 3's
+# additive mix64(key) ^ d; 2 = mix64(mix64(key) ^ d), mixed after combining (round 4).  A file
+# without this key, or with another value, is never resumed from or merged into.
+DIGEST_FORMAT = bench.DIGEST_FORMAT
 CASES = [("c1", 0)] + [("c2", s) for s in range(RANKS)] + [("c3", 0), ("c4", 0)] + [("c4", s) for s in range(1, RANKS)] + [("c5", 0)]
 
 
@@ -58,7 +63,14 @@ def main():
     resume = bool(os.environ.get("MP2VG_DIGESTS_RESUME"))
     if (only or resume) and os.path.exists(path):
         with np.load(path) as d:
-            out = {k: d[k].copy() for k in d.files}
+            fmt = int(d["digest_format"][0]) if "digest_format" in d.files else 1
+            if fmt != DIGEST_FORMAT:
+                if only:
+                    sys.exit(f"{path} holds digest format {fmt}, not {DIGEST_FORMAT}: regenerate every config")
+                print(f"{path}: digest format {fmt} != {DIGEST_FORMAT}, starting over")
+            else:
+                out = {k: d[k].copy() for k in d.files}
+    out["digest_format"] = np.array([DIGEST_FORMAT], np.int64)
     with tempfile.TemporaryDirectory() as tmp:
         for config, rank in CASES:
             if only and config not in only:

@@ -277,6 +277,10 @@ def test_reference_digests_for_every_rank_of_the_scaling_run(config, ranks):
     import sys
     sys.path[:0] = [REPO]
     import bench
+    import numpy as np
+    with np.load(os.path.join(REPO, "tests", "golden", "bench_digests.npz")) as d:
+        # the entries were computed with the formula bench.py's device digests use
+        assert int(d["digest_format"][0]) == bench.DIGEST_FORMAT
     for r in range(ranks):
         exp = bench.expected_digests(config, bench.DEFAULT_GOPS[config], 1729 + r)
         assert exp is not None and len(exp) == 12 * bench.DEFAULT_GOPS[config], (config, r)

@@ -182,6 +182,41 @@ def test_anchor_tiles_across_batches(cf):
                 assert np.array_equal(got[k], exp[p][k]), (p, k)
 
 
+def test_external_reference_write_then_invalidate():
+    """A reference slot written from outside the decode (here a device-to-device copy of another
+    context's decoded I picture through mp2vg_slot_device_ptr, as an RCCL receive would) is seen
+    by later predictions only after mp2vg_invalidate_slot: the taps read the slot's anchor tiles,
+    which the invalidated slot gets rebuilt from its frame before the next batch reads it."""
+    import ctypes
+    from tiny_mp2v_dec_amd import _lib
+    from tiny_mp2v_dec_amd.decoder import _hip_lib
+    w, h, cf = 96, 64, 1
+    pics, mbs, coefs = random_batch(w, h, cf, 3, seed=777)
+    exp = oracle_frames(_P(w, h, cf, pics, mbs, coefs))
+    n = (w // 16) * (h // 16)
+    c0 = int(mbs["coef_off"][n])
+    rest, mrest = pics[1:].copy(), mbs[n:].copy()
+    rest["mb_first"] -= n
+    mrest["coef_off"] -= c0
+    with R.DeviceContext(w, h, cf, slots=3) as src, R.DeviceContext(w, h, cf, slots=3) as dst:
+        src.upload(pics[:1], mbs[:n], coefs[:c0])  # the I picture, decoded into src's slot 0
+        src.decode()
+        src.synchronize()
+        ps, pd = ctypes.c_void_p(), ctypes.c_void_p()
+        _lib.check(_lib.lib().mp2vg_slot_device_ptr(src.h, 0, ctypes.byref(ps)), "slot_device_ptr")
+        _lib.check(_lib.lib().mp2vg_slot_device_ptr(dst.h, 0, ctypes.byref(pd)), "slot_device_ptr")
+        assert _hip_lib().hipMemcpy(pd.value, ps.value, int(src.slot_bytes), 3) == 0  # device to device
+        _lib.check(_lib.lib().mp2vg_invalidate_slot(dst.h, 0), "invalidate_slot")
+        with pytest.raises(_lib.Mp2vgError):
+            _lib.check(_lib.lib().mp2vg_invalidate_slot(dst.h, 3), "invalidate_slot")
+        dst.upload(rest, mrest, coefs[c0:])  # the P and B pictures predict from slot 0
+        dst.decode()
+        dst.synchronize()
+        for p in range(3):
+            got = dst.download(p)
+            assert all(np.array_equal(got[k], exp[p][k]) for k in range(3)), p
+
+
 def test_full_size_1080p_digest_vs_oracle():
     """BASELINE config size (1920x1088 4:2:0, one closed GOP of the §8d C2 mix): device digest of
     every frame == host digest of the oracle's frames (size-independent checksum-of-checksums)."""

@@ -59,6 +59,12 @@ def test_malformed_batches_rejected():
     bad(mbs=mbs, match="outside the batch")
     pics = p.pics.copy(); pics[1]["fwd_slot"] = -1; pics[1]["bwd_slot"] = -1
     bad(pics=pics, match="missing reference")
+    # the picture type picks the launch's kernel mode and whether the picture stores anchor
+    # tiles (runtime.cpp TilePlan): a type outside 1..3 would run the B kernel without storing the
+    # tiles a later picture reads
+    for t in (0, 4, -1):
+        pics = p.pics.copy(); pics[1]["picture_coding_type"] = t
+        bad(pics=pics, match="picture_coding_type")
     R.validate_batch(*args, p.pics, p.mbs, p.coefs)
 
 

@@ -58,16 +58,25 @@ static int default_streams(const mp2vg_config_t* cfg) {
 // Bytes between consecutive frame slots beyond the slot itself (MP2VG_SLOT_PAD overrides for the
 // pool-placement measurements, profiles/r4/README.md): slot offsets decide which HBM channels the
 // same pixel rows of different pictures land on.
+// (Dev builds only, -DMP2VG_DEV_ABLATIONS: a product library ignores these variables.)
+static const char* dev_env(const char* name) {
+#ifdef MP2VG_DEV_ABLATIONS
+    return getenv(name);
+#else
+    (void)name;
+    return nullptr;
+#endif
+}
 static size_t slot_pad() {
-    const char* e = getenv("MP2VG_SLOT_PAD");
+    const char* e = dev_env("MP2VG_SLOT_PAD");
     return e ? (size_t)std::max(0, atoi(e)) & ~(size_t)255 : 0;
 }
 static size_t tile_pad() {  // the same for the anchor-tile slots (MP2VG_TILE_PAD)
-    const char* e = getenv("MP2VG_TILE_PAD");
+    const char* e = dev_env("MP2VG_TILE_PAD");
     return e ? (size_t)std::max(0, atoi(e)) & ~(size_t)255 : 0;
 }
 static int set_coupling() {
-    const char* e = getenv("MP2VG_SET_COUPLE");
+    const char* e = dev_env("MP2VG_SET_COUPLE");
     return e ? atoi(e) : 0;
 }
 
@@ -311,38 +320,55 @@ extern "C" int mp2vg_reserve_slots(mp2vg_ctx_t* c, int32_t nslots) {
     // (profiles/r4/README.md, placement).
     static const int chunk = getenv("MP2VG_POOL_CHUNK") ? std::max(0, atoi(getenv("MP2VG_POOL_CHUNK"))) : 16;
     if (chunk > 0) {
+        // the new blocks are committed to the context only once every allocation has succeeded: a
+        // failed reserve leaves the pool (chunks, fptr, tptr, nslots) as it was, and frees its blocks
+        std::vector<uint8_t*> blocks;
+        std::vector<uint64_t> fp, tp;
+        auto fail = [&](hipError_t e) {
+            for (uint8_t* q : blocks) hipFree(q);
+            set_error(std::string("hipMalloc (frame pool block): ") + hipGetErrorString(e));
+            return MP2VG_E_HIP;
+        };
         for (int s0 = c->nslots; s0 < nslots; s0 += chunk) {
             const int k = std::min(chunk, nslots - s0);
             uint8_t *f = nullptr, *t = nullptr;
-            HIPCHK(hipMalloc((void**)&f, c->slot_stride * k + kPoolPad));
-            c->chunks.push_back(f);
-            HIPCHK(hipMalloc((void**)&t, c->tile_stride * k));
-            c->chunks.push_back(t);
-            HIPCHK(hipMemsetAsync(f, 0, c->slot_stride * k + kPoolPad, c->stream));
-            HIPCHK(hipMemsetAsync(t, 0, c->tile_stride * k, c->stream));
+            hipError_t e = hipMalloc((void**)&f, c->slot_stride * k + kPoolPad);
+            if (e != hipSuccess) return fail(e);
+            blocks.push_back(f);
+            if ((e = hipMalloc((void**)&t, c->tile_stride * k)) != hipSuccess) return fail(e);
+            blocks.push_back(t);
+            if ((e = hipMemsetAsync(f, 0, c->slot_stride * k + kPoolPad, c->stream)) != hipSuccess ||
+                (e = hipMemsetAsync(t, 0, c->tile_stride * k, c->stream)) != hipSuccess)
+                return fail(e);
             for (int i = 0; i < k; i++) {
-                c->fptr.push_back((uint64_t)(uintptr_t)(f + (size_t)i * c->slot_stride));
-                c->tptr.push_back((uint64_t)(uintptr_t)(t + (size_t)i * c->tile_stride));
+                fp.push_back((uint64_t)(uintptr_t)(f + (size_t)i * c->slot_stride));
+                tp.push_back((uint64_t)(uintptr_t)(t + (size_t)i * c->tile_stride));
             }
         }
+        c->chunks.insert(c->chunks.end(), blocks.begin(), blocks.end());
+        c->fptr.insert(c->fptr.end(), fp.begin(), fp.end());
+        c->tptr.insert(c->tptr.end(), tp.begin(), tp.end());
         return finish_reserve(c, nslots);
     }
     uint8_t* p = nullptr;
     uint8_t* t = nullptr;
     size_t bytes = c->slot_stride * nslots + kPoolPad;
     const size_t tbytes = c->tile_stride * nslots;
+#ifdef MP2VG_DEV_ABLATIONS
     // dev knob for the pool-placement study (profiles/r4/README.md): 1 = physically contiguous
-    // (hipDeviceMallocContiguous, default allocation if the driver refuses it)
+    // (hipDeviceMallocContiguous, default allocation if the driver refuses it); 5 = the process's
+    // first block (pool-sized, or MP2VG_BALLAST_MB) is held for good.  Dev builds only.
     static const int pool_alloc = getenv("MP2VG_POOL_ALLOC") ? atoi(getenv("MP2VG_POOL_ALLOC")) : 0;
     if (pool_alloc == 1 && hipExtMallocWithFlags((void**)&p, bytes, hipDeviceMallocContiguous) != hipSuccess) {
         (void)hipGetLastError();
         p = nullptr;
     }
-    static uint8_t* ballast = nullptr;  // 5: the process's first block (pool-sized, or MP2VG_BALLAST_MB) is held for good
+    static uint8_t* ballast = nullptr;
     static const size_t ballast_mb = getenv("MP2VG_BALLAST_MB") ? (size_t)atoll(getenv("MP2VG_BALLAST_MB")) : 0;
     if (pool_alloc == 5 && !ballast &&
         hipMalloc((void**)&ballast, ballast_mb ? ballast_mb << 20 : bytes + tbytes) != hipSuccess)
         (void)hipGetLastError(), ballast = nullptr;
+#endif
     if (!p) HIPCHK(hipMalloc((void**)&p, bytes));
     if (hipMalloc((void**)&t, tbytes) != hipSuccess) {
         hipFree(p);
@@ -392,8 +418,12 @@ static int plan_batch(mp2vg_ctx_t* c, const mp2vg_picture_t* pics, int32_t npics
     // records of this library's own parser (the drop-in decoder) meet the contract by
     // construction (tests/test_validate.py: parsed batches validate): only the picture-level checks
     // and the reference usage the scheduler needs are computed for them
+    // the picture type picks the kernel mode of its launch and whether it stores anchor tiles
+    // (TilePlan): only 1 (I), 2 (P) and 3 (B) exist (mp2vg.h)
+    auto bad_type = [&](int p) { return pics[p].picture_coding_type < 1 || pics[p].picture_coding_type > 3; };
     auto uses_only = [&](int p) -> const char* {
         const mp2vg_picture_t& P = pics[p];
+        if (bad_type(p)) return "picture_coding_type is not 1 (I), 2 (P) or 3 (B)";
         if (P.mb_width != mbw || P.mb_height != mbh) return "picture size differs from the context geometry";
         if (P.dst_slot < 0 || P.dst_slot >= c->nslots || P.fwd_slot >= c->nslots || P.bwd_slot >= c->nslots)
             return "frame slot out of range (mp2vg_reserve_slots)";
@@ -418,6 +448,7 @@ static int plan_batch(mp2vg_ctx_t* c, const mp2vg_picture_t* pics, int32_t npics
     auto validate = [&](int p) -> const char* {
         if (trusted) return uses_only(p);
         const mp2vg_picture_t& P = pics[p];
+        if (bad_type(p)) return "picture_coding_type is not 1 (I), 2 (P) or 3 (B)";
         if (P.mb_width != mbw || P.mb_height != mbh) return "picture size differs from the context geometry";
         if (P.dst_slot < 0 || P.dst_slot >= c->nslots || P.fwd_slot >= c->nslots || P.bwd_slot >= c->nslots)
             return "frame slot out of range (mp2vg_reserve_slots)";
@@ -970,6 +1001,12 @@ extern "C" int mp2vg_copy_slot_packed(mp2vg_ctx_t* c, int32_t slot, void* dst, i
         d += (size_t)c->g.pw[p] * c->g.ph[p];
     }
     HIPCHK(hipStreamSynchronize(c->stream));
+    return MP2VG_OK;
+}
+
+extern "C" int mp2vg_invalidate_slot(mp2vg_ctx_t* c, int32_t slot) {
+    if (!c || slot < 0 || slot >= c->nslots) return MP2VG_E_INVALID;
+    c->tiles_ok[slot] = 0;  // mp2vg_batch_decode rebuilds them before a batch reads the slot
     return MP2VG_OK;
 }
 
