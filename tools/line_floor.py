@@ -133,6 +133,34 @@ def picture_taps(P, mbs, stride, ph, plane_off, cf, layout, luma=True):
                 nbytes = 20 if pw == 16 else (12 if pw == 8 else 20)
                 sel = np.broadcast_to(u[:, None], Y.shape)
                 gid = np.broadcast_to(grp[:, None], Y.shape)
+                if layout == "apron_h8" and plane == 0:
+                    step = np.broadcast_to(step, Y.shape)
+                    # half-row luma lanes (MB, r < 8, half h): instruction A = rows r, B = rows
+                    # r + 8, E = the rows past 15 for the wrap lanes (r + step > 7) with vertical
+                    # half-pel; one 12-B (b96) load per half row inside its apron tile row
+                    for part, (rsel, msel) in enumerate((("A", None), ("B", None), ("E", None))):
+                        for hh in range(2):
+                            Xh = X + 8 * hh
+                            if part == 0:
+                                rows_, m_ = Y[:, :8], sel[:, :8]
+                            elif part == 1:
+                                rows_, m_ = Y[:, 8:], sel[:, 8:]
+                            else:
+                                rows_ = Y[:, 8:] + step[:, 8:]
+                                wrap = (np.arange(8)[None, :] + step[:, 8:]) > 7
+                                m_ = sel[:, 8:] & hy[:, 8:] & wrap
+                            X0 = (Xh[:, :8] if part == 0 else Xh[:, 8:]) & ~3
+                            XL = (X[:, :8] if part == 0 else X[:, 8:]) & ~3  # both halves in the left half's tile
+                            t = (rows_ // 4) * -(-st // 16) + (XL // 16)
+                            a = t * 128 + (rows_ % 4) * 32 + (X0 - 16 * (XL // 16))
+                            m = m_.ravel()
+                            ids = (np.broadcast_to(grp[:, None], rows_.shape).ravel() * 64 + kind * 4 + part)[m]
+                            for addr in (a.ravel()[m], a.ravel()[m] + 11):
+                                out_ids.append(ids)
+                                out_lines.append(addr >> 7)
+                                out_sec.append(addr >> 6)
+                    kind += 1
+                    continue
                 for part, (rows, mask) in enumerate(((Y, sel), (Y + step, sel & hy & edge))):
                     X0 = X & ~3
                     if layout == "linear":
@@ -141,7 +169,7 @@ def picture_taps(P, mbs, stride, ph, plane_off, cf, layout, luma=True):
                     elif layout.startswith("apron"):  # one load per row inside a tile row with its apron
                         # apron: 4 rows x (16 + 16 apron) luma, 8 x (8 + 8) chroma (recon.hip tile_off);
                         # apron2: 2 rows x (48 + 16 apron) luma, 4 x (24 + 8) chroma (1.33x the bytes)
-                        R_, OW = ((4, 16), (8, 8)) [plane > 0] if layout == "apron" else ((2, 48), (4, 24))[plane > 0]
+                        R_, OW = ((4, 16), (8, 8)) [plane > 0] if layout in ("apron", "apron_h8") else ((2, 48), (4, 24))[plane > 0]
                         t = (rows // R_) * -(-st // OW) + (X0 // OW)
                         a = (1 << 40) * plane + t * 128 + (rows % R_) * (128 // R_) + (X0 % OW)
                         spans = [(a, a + min(nbytes, 16) - 1, 0)] + ([(a + 16, a + nbytes - 1, 1)] if nbytes > 16 else [])
@@ -175,7 +203,8 @@ def main():
     plane_off = [0, stride[0] * ph[0], stride[0] * ph[0] + stride[1] * ph[1]]
     n = int(parsed.pics[0]["mb_width"]) * int(parsed.pics[0]["mb_height"])
     res = {}
-    for layout in ("linear", "apron", "apron2", "tile8x16", "luma2d_tw8", "luma2d_tw4"):
+    for layout in (sys.argv[sys.argv.index("--layouts") + 1].split(",") if "--layouts" in sys.argv else
+                   ("linear", "apron", "apron2", "apron_h8", "tile8x16", "luma2d_tw8", "luma2d_tw4")):
         ta_l = ta_s = grp_l = groups = 0
         for p in range(parsed.npics):
             P = parsed.pics[p]

@@ -28,12 +28,23 @@ def main(d):
             k = kname(r["Kernel_Name"])
             if k:
                 rows[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    # per-kernel durations from the kernel trace, without onestream.py's warm-up batch (its first
+    # launches per level): the same launches the tool's HIP-event table averages
     stats = {}
-    for f in glob.glob(os.path.join(d, "ktrace", "*kernel_stats.csv")):
-        for r in csv.DictReader(open(f)):
-            k = kname(r["Name"])
-            if k:
-                stats[k] = (int(r["Calls"]), float(r["AverageNs"]) / 1e6, float(r["MinNs"]) / 1e6, float(r["MaxNs"]) / 1e6)
+    for f in glob.glob(os.path.join(d, "ktrace", "*kernel_trace.csv")):
+        disp = sorted((int(r["Correlation_Id"]), kname(r["Kernel_Name"]), int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+                      for r in csv.DictReader(open(f)) if kname(r["Kernel_Name"]))
+        ev0 = None
+        for line in open(os.path.join(d, "ktrace.log")) if os.path.exists(os.path.join(d, "ktrace.log")) else []:
+            if line.startswith("{"):
+                ev0 = json.loads(line)
+        nl = sum(v["launches_per_batch"] for v in ev0["per_kernel"].values()) if ev0 else 5
+        timed = disp[nl:]
+        by = collections.defaultdict(list)
+        for _, k, ns in timed:
+            by[k].append(ns / 1e6)
+        for k, v in by.items():
+            stats[k] = (len(v), sum(v) / len(v), min(v), max(v))
     ev = None
     log = os.path.join(d, "ktrace.log")
     if os.path.exists(log):
@@ -44,8 +55,8 @@ def main(d):
     if ev:
         print(f"config {ev['config']}, {ev['gops']} GOPs, {ev['frames']} frames per batch, parity {ev['parity']}, "
               f"one-stream batch span {ev['span_ms']} ms (HIP events)\n")
-    print("| kernel | mode | calls | rocprof mean ms (min / max) | HIP-event mean ms | algorithmic bytes | frac (rocprof mean) |")
-    print("|---|---|---|---|---|---|---|")
+    print("| kernel | mode | timed dispatches | rocprof mean ms (min / max) | HIP-event mean ms | rocprof / events | algorithmic bytes | frac (rocprof mean) |")
+    print("|---|---|---|---|---|---|---|---|")
     for k in sorted(stats):
         calls, avg, mn, mx = stats[k]
         e = None
@@ -53,8 +64,9 @@ def main(d):
             e = next((v for n, v in ev["per_kernel"].items() if n.replace(" ", "").replace("recon_kernel", "") == k), None)
         ab = e["algorithmic_bytes_per_launch"] if e else None
         frac = f"{ab / (avg / 1e3) / 8.0e12:.4f}" if ab else "-"
+        ratio = f"{avg / e['avg_launch_ms']:.3f}" if e else "-"
         print(f"| `recon_kernel{k}` | {e['mode'] if e else '-'} | {calls} | {avg:.4f} ({mn:.4f} / {mx:.4f}) | "
-              f"{e['avg_launch_ms'] if e else '-'} | {ab} | {frac} |")
+              f"{e['avg_launch_ms'] if e else '-'} | {ratio} | {ab} | {frac} |")
     print()
     for k in sorted(rows):
         c = {n: sum(v) / len(v) for n, v in rows[k].items()}
