@@ -357,6 +357,11 @@ int  mp2vg_decoder_lane_frames(const mp2vg_decoder_t* dec, int32_t* frames, int3
 /* frame buffers the decoder's frame pools hold (host + device): 2 * 16 + 4 per lane unless a
  * renderer that holds no frame had to wait for display order (then the pool grows) */
 int  mp2vg_decoder_frames_allocated(const mp2vg_decoder_t* dec);
+/* lane hand-offs in the last decode() (several lanes): in_flight = times the stream moved to
+ * another lane while the lane just left was still downloading its last chunk (the host did not
+ * wait: both lanes' chunks in flight at once); blocks = times the host waited for another lane's
+ * downloads because the frame pool could not give the next chunk its frames otherwise */
+int  mp2vg_decoder_handoff_stats(const mp2vg_decoder_t* dec, int32_t* in_flight, int32_t* blocks);
 int  mp2vg_decoder_destroy(mp2vg_decoder_t* dec);
 
 #ifdef __cplusplus

@@ -170,6 +170,39 @@ def test_dropin_gop_sharding_over_device_lanes(devices):
     assert lanes == [sum(runs[r] for r in range(i, len(runs), n)) for i in range(n)]
 
 
+def test_dropin_lane_handoff_does_not_wait_for_the_lane_left():
+    """A lane change no longer blocks the host on the lane just left (decoder.cpp: its last chunk
+    stays in flight until its downloads have landed, checked without waiting; the host waits on
+    another lane only when the frame pool could not give the next chunk its frames).  1080p
+    frames over three lanes on the one GPU: every lane change is either left in flight or
+    completed without a wait, frames are the oracle's in display order (digests), and the pool
+    keeps its reserved size."""
+    from tiny_mp2v_dec_amd.records import generate_es
+    import numpy as np
+    from tiny_mp2v_dec_amd import records as R
+    es = generate_es(width=1920, height=1088, chroma_format=1, n_gops=6, gop_n=12, gop_m=3, seed=71)
+    parsed = R.Parsed(es, 1920, 1088, 1)
+    from helpers import oracle_frames
+    exp_frames = oracle_frames(parsed)
+    exp = [R.planes_digest(exp_frames[d]) for d in parsed.display]
+    got = []
+
+    def render(f):
+        got.append(R.planes_digest([np.array(f.get_planes(i)[:, :f.get_width(i)]) for i in range(3)]))
+
+    dec = mp2v_decoder_c(decoder_config_t(1920, 1088, 1, num_threads=6, devices=[0, 0, 0]), render)
+    before = dec.frames_allocated()
+    dec.decode(es)
+    in_flight, blocks = dec.handoff_stats()
+    after = dec.frames_allocated()
+    lanes = dec.lane_frames()
+    dec.close()
+    assert got == exp
+    assert after == before
+    assert lanes == [24, 24, 24]  # three runs of two 12-picture GOPs
+    assert 0 <= in_flight <= 2 and 0 <= blocks <= 2  # two lane changes
+
+
 def test_dropin_lanes_long_gops_bounded_pool_and_i_only():
     """Two lanes on long closed GOPs (96 pictures, longer than the 72-frame pool) keep the frame pool
     at its reserved size -- a lane's last chunk completes when the stream moves to the other lane,

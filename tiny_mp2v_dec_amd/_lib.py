@@ -115,7 +115,8 @@ EXPORTS = [
     "mp2vg_parsed_shards", "mp2vg_parsed_free", "mp2vg_vlc_decode",
     "mp2vg_gen_default_params", "mp2vg_generate_es", "mp2vg_free", "mp2vg_decoder_create",
     "mp2vg_decoder_create_multi", "mp2vg_decoder_decode", "mp2vg_decoder_stream_headers",
-    "mp2vg_decoder_lane_frames", "mp2vg_decoder_frames_allocated", "mp2vg_decoder_destroy",
+    "mp2vg_decoder_lane_frames", "mp2vg_decoder_frames_allocated", "mp2vg_decoder_handoff_stats",
+    "mp2vg_decoder_destroy",
 ]
 
 _lib = None
@@ -172,6 +173,7 @@ def lib():
         "mp2vg_decoder_stream_headers": ([VP, P(StreamHeaders)], ctypes.c_int),
         "mp2vg_decoder_lane_frames": ([VP, P(I32), I32], ctypes.c_int),
         "mp2vg_decoder_frames_allocated": ([VP], ctypes.c_int),
+        "mp2vg_decoder_handoff_stats": ([VP, P(I32), P(I32)], ctypes.c_int),
         "mp2vg_decoder_destroy": ([VP], ctypes.c_int),
     }
     for name, (args, res) in sig.items():

@@ -115,6 +115,10 @@ class FramePool {
         }
         cv_.notify_all();
     }
+    size_t free_count() {
+        std::lock_guard<std::mutex> lk(mu_);
+        return free_.size();
+    }
     size_t size() {
         std::lock_guard<std::mutex> lk(mu_);
         return all_.size();
@@ -184,6 +188,7 @@ struct Lane {
     std::vector<int> free_slots;
     std::map<int, HostFrame*> inflight;  // decode index -> frame whose copy is in flight
     std::vector<int> pend;               // pictures of the chunk whose copies are in flight
+    uint64_t pend_seq = 0;               // chunk number of `pend` (oldest pending lane first)
     std::vector<int> held;               // copied pictures whose slot a later picture still reads
     ~Lane() {
         hipSetDevice(device);
@@ -211,6 +216,10 @@ struct mp2vg_decoder {
     // device it was allocated under; lanes on several devices copy by DMA)
     bool kernel_copy = false;
     mp2vg_stream_headers_t hdrs{};     // of the last decode()
+    // of the last decode(): lane changes that found the lane just left still downloading (its
+    // chunk left in flight, the host moving on), and host blocks on another lane's downloads
+    // (only when the frame pool runs short)
+    int handoffs_in_flight = 0, handoff_blocks = 0;
 };
 
 extern "C" int mp2vg_decoder_destroy(mp2vg_decoder_t* d) {
@@ -311,6 +320,13 @@ extern "C" int mp2vg_decoder_lane_frames(const mp2vg_decoder_t* d, int32_t* fram
     if (!d) return MP2VG_E_INVALID;
     for (int i = 0; i < n && i < (int)d->lanes.size(); i++) frames[i] = d->lanes[i]->frames;
     return (int)d->lanes.size();
+}
+
+extern "C" int mp2vg_decoder_handoff_stats(const mp2vg_decoder_t* d, int32_t* in_flight, int32_t* blocks) {
+    if (!d) return MP2VG_E_INVALID;
+    if (in_flight) *in_flight = d->handoffs_in_flight;
+    if (blocks) *blocks = d->handoff_blocks;
+    return MP2VG_OK;
 }
 
 extern "C" int mp2vg_decoder_frames_allocated(const mp2vg_decoder_t* d) {
@@ -601,19 +617,49 @@ extern "C" int mp2vg_decoder_decode(mp2vg_decoder_t* d, const uint8_t* buf, uint
         return MP2VG_OK;
     };
 
+    // a lane's pending chunk is completed without blocking when its downloads have all landed
+    auto try_complete = [&](Lane& X) -> int {
+        if (X.pend.empty()) return MP2VG_OK;
+        hipSetDevice(X.device);
+        for (int i = 0; i < X.ndl; i++) {
+            const hipError_t q = hipStreamQuery(X.dl[i]);
+            if (q == hipErrorNotReady) return 1;
+            if (q != hipSuccess) return MP2VG_E_HIP;
+        }
+        return complete_pending(X);
+    };
     // chunks: up to kChunk consecutive pictures of one lane; with several lanes a chunk also ends
     // where the stream moves to the next shard's lane, so the chunks (and the parse window) still
     // advance in decode order and every lane decodes while the next one is being fed
     Lane* prev = nullptr;
+    uint64_t seq = 0;
+    d->handoffs_in_flight = d->handoff_blocks = 0;
     for (int s = 0; s < npics;) {
         Lane& L = lane_of(s);
         int e = s + 1;
         while (e < npics && e - s < kChunk && (nl == 1 || &lane_of(e) == &L)) e++;
+        // other lanes whose downloads have landed hand their frames on (display order) without a
+        // wait; one still downloading keeps its chunk in flight while this lane is fed, so with
+        // several lanes every lane's chunk can be in flight at once.  Only when the frame pool
+        // could not give this chunk its frames without growing does the host wait, for the
+        // oldest pending lane first (its frames come first in display order).
+        if (nl > 1) {
+            for (auto& Xp : d->lanes)
+                if (Xp.get() != &L && (rc = try_complete(*Xp)) < 0) return finish(rc);
+            FramePool& pool = d->device_frames ? *L.dpool : *d->hpool;
+            for (;;) {
+                if (pool.free_count() >= (size_t)(e - s)) break;
+                Lane* old = nullptr;
+                for (auto& Xp : d->lanes)
+                    if (Xp.get() != &L && !Xp->pend.empty() && (!old || Xp->pend_seq < old->pend_seq)) old = Xp.get();
+                if (!old) break;
+                d->handoff_blocks++;
+                if ((rc = complete_pending(*old)) != MP2VG_OK) return finish(rc);
+            }
+        }
         if ((rc = run_chunk(L, s, e)) != MP2VG_OK) return finish(rc);
-        // the lane just left finishes its last chunk now (this lane's chunk is already queued):
-        // otherwise its frames wait in flight until it runs again, display order stalls behind
-        // them, and the renderer idles while the frame pool grows
-        if (prev && prev != &L && (rc = complete_pending(*prev)) != MP2VG_OK) return finish(rc);
+        L.pend_seq = seq++;
+        if (prev && prev != &L && !prev->pend.empty()) d->handoffs_in_flight++;
         prev = &L;
         s = e;
     }

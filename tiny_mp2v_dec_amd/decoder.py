@@ -163,6 +163,13 @@ class mp2v_decoder_c:  # noqa: N801  (reference name)
         lib().mp2vg_decoder_lane_frames(self._h, out, n)
         return list(out)
 
+    def handoff_stats(self):
+        """(lane changes that left the previous lane's chunk in flight, host waits on another
+        lane's downloads) in the last decode() (mp2vg_decoder_handoff_stats)."""
+        a, b = ctypes.c_int32(), ctypes.c_int32()
+        lib().mp2vg_decoder_handoff_stats(self._h, ctypes.byref(a), ctypes.byref(b))
+        return a.value, b.value
+
     def frames_allocated(self):
         """Frame buffers held by the decoder's frame pools (bounded: the renderer back-pressures
         the decoder as the reference's fixed picture pool does)."""
