@@ -142,9 +142,12 @@ class _P:  # minimal Parsed-like holder for oracle_frames
 
 @pytest.mark.parametrize("cf", [1, 2, 3])
 @pytest.mark.parametrize("big", [False, True])
-def test_random_records_vs_oracle(cf, big):
-    """Synthetic record batches (all MB kinds, field MC / DCT, saturating levels) vs the oracle."""
-    w, h = 96, 64
+@pytest.mark.parametrize("size", [(96, 64), (128, 48)], ids=["6mb_rows", "8mb_rows"])
+def test_random_records_vs_oracle(cf, big, size):
+    """Synthetic record batches (all MB kinds, field MC / DCT, saturating levels) vs the oracle.
+    8-MB rows (a multiple of the kernel's 4-MB group): the P/B launches' workgroups take two MB
+    rows each (runtime.cpp plan_batch), three rows leave a one-row last slice."""
+    w, h = size
     pics, mbs, coefs = random_batch(w, h, cf, 5, seed=1729 + cf + 10 * big, big=big)
     exp = oracle_frames(_P(w, h, cf, pics, mbs, coefs))
     got = gpu_decode(_P(w, h, cf, pics, mbs, coefs))

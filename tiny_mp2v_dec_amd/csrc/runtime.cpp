@@ -619,6 +619,15 @@ static int plan_batch(mp2vg_ctx_t* c, const mp2vg_picture_t* pics, int32_t npics
     }
     slices.clear();
     launches.clear();
+    // MB rows per workgroup (the kernel's "slice"): 2 in launches with P/B pictures, 1 in I-only
+    // launches.  A 1080p row is 30 four-MB groups, 8/8/7/7 over a workgroup's four waves, so two
+    // of them idle for the row's last iteration; two rows are 15 groups per wave, and half as many
+    // pipeline ramps.  Measured (c2, same box, 2 rounds, profiles/r5/README.md): 2 rows +2.4 %
+    // (355.4k -> 363.9k frames/s), 3 rows +1.6 %; the I kernel prefers 1 row (c1 -2 % with 2).
+    // Groups never straddle rows when the row is a multiple of 4 MBs; other widths keep 1 row.
+    // (MP2VG_SLICE_ROWS / MP2VG_SLICE_ROWS_I override in dev builds.)
+    static const int rows_pb = dev_env("MP2VG_SLICE_ROWS") ? std::max(1, atoi(dev_env("MP2VG_SLICE_ROWS"))) : 2;
+    static const int rows_i = dev_env("MP2VG_SLICE_ROWS_I") ? std::max(1, atoi(dev_env("MP2VG_SLICE_ROWS_I"))) : 1;
     for (int set = 0; set < nsets; set++)
     for (int q = 0; q <= maxlevel; q++) {
         std::vector<int> lp;
@@ -647,10 +656,11 @@ static int plan_batch(mp2vg_ctx_t* c, const mp2vg_picture_t* pics, int32_t npics
                 if (!share) break;
                 j++;
             }
-            for (int r = 0; r < mbh; r++)
+            const int slice_rows = (mbw % 4 != 0) ? 1 : (types == 1 ? rows_i : rows_pb);
+            for (int r = 0; r < mbh; r += slice_rows)
                 for (size_t k = i; k < j; k++)
-                    slices.push_back({(uint32_t)lp[k], pics[lp[k]].mb_first + (uint32_t)(r * mbw), (uint32_t)mbw,
-                                      need[lp[k]]});
+                    slices.push_back({(uint32_t)lp[k], pics[lp[k]].mb_first + (uint32_t)(r * mbw),
+                                      (uint32_t)(std::min(slice_rows, mbh - r) * mbw), need[lp[k]]});
             i = j;
         }
         l.end = (uint32_t)slices.size();
