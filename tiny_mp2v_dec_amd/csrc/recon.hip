@@ -190,7 +190,13 @@ __device__ __forceinline__ int left_block(int plane, int py, bool dctf) {
 
 constexpr int WAVES = 4;
 constexpr int G = 4;               // macroblocks per wave group
-constexpr int STEP = WAVES * G;    // a wave's next group starts STEP MBs later
+// waves per workgroup of the I kernels (MP2VG_I_WAVES, round-5 A/B; the P/B kernels keep WAVES):
+// a 1080p row is 30 groups, 8/8/7/7 over 4 waves, 5/5/5/5/5/5 over 6
+#ifndef MP2VG_I_WAVES
+#define MP2VG_I_WAVES 4
+#endif
+template <int MCM, int ABL>
+constexpr int kernel_waves() { return MCM == 0 && ABL == 0 ? MP2VG_I_WAVES : WAVES; }
 
 // Residual image of one MB in LDS (int16): luma 16x16, then Cb CW x CH, then Cr.  Inside each
 // group of 4 pixels the order is x0, x0+2, x0+1, x0+3: one v_perm unpacks the matching
@@ -760,20 +766,22 @@ __device__ __forceinline__ void tile_group(uint32_t mx0, uint32_t mby, int lane,
 constexpr int BLKS = 72;
 // C8 = the compact layout of the I kernels (4:4:4: 38.4 KB instead of 53.8 KB per workgroup, so
 // four workgroups share a CU instead of three; 4:2:2 26.0 KB, 4:2:0 19.9 KB)
-template <int CF, bool C8 = false>
+template <int CF, bool C8 = false, int NWV = WAVES>
 struct Lds {
     static constexpr bool COMPACT = C8;
+    static constexpr int NWAVES = NWV;           // waves per workgroup
+    static constexpr int STEP = NWV * G;         // a wave's next group starts STEP MBs later
     static constexpr int MAXS = G * Fmt<CF>::NB;  // coded-block slots per group
     // coef raster -> pass-1 out.  Slots 144 B apart (BLK = 72 shorts): the transposed pass-1
     // writes of the 8 slots in a 32-lane half then hit distinct banks (128 B apart: 8-way
     // conflicts).  C8: slots 128 B apart with the 16-B chunk index XOR (slot & 7), same banks.
     static constexpr int BLK = C8 ? 64 : BLKS;
-    short blk[WAVES][MAXS][BLK];
+    short blk[NWV][MAXS][BLK];
     // residual images, int16 in ResLayout; C8 (intra only: output = clamp(residual)): the clamped
     // pixels as bytes in the same ResLayout order, half the size
-    short res[WAVES][C8 ? G * ResLayout<CF>::SIZE / 2 : G * ResLayout<CF>::SIZE];
-    uint8_t map[WAVES][MAXS];                    // slot -> k*16 + b
-    uint32_t dq[WAVES][64];                      // (k*16 + b) -> dequant parameters (DqEntry)
+    short res[NWV][C8 ? G * ResLayout<CF>::SIZE / 2 : G * ResLayout<CF>::SIZE];
+    uint8_t map[NWV][MAXS];                      // slot -> k*16 + b
+    uint32_t dq[NWV][64];                        // (k*16 + b) -> dequant parameters (DqEntry)
     uint8_t W[4][64];
     // I kernels (WB): the intra matrix row of each block b (W[0] for b < 6, W[2] above), so a
     // coefficient word's (b, i) bits 16-25 index it directly; scan positions stored doubled (byte
@@ -1015,6 +1023,7 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, LT&
     using F = Fmt<CF>;
     using RL = ResLayout<CF>;
     constexpr int NB = F::NB;
+    constexpr int STEP = LT::STEP;
     constexpr int NWC = F::CW / 4;
     // 4:2:0 intra groups (24 blocks) run both IDCT passes in shared rounds (D' below)
     constexpr bool UNI = LT::COMPACT && CF == 1;
@@ -1144,6 +1153,10 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, LT&
         wave_sync();
 
         stamp<ABL>(st, 2);
+        // dev ablations (timing only): IDCT pass 2 (131072) or both passes (262144) skipped in
+        // every second group of the wave -- the bound of pooling two groups' IDCT rounds
+        bool odd = false;
+        if constexpr ((ABL & (131072 | 262144)) != 0) odd = ((g - c.mb_begin) / STEP) & 1;
         if constexpr (!UNI) {
             // ---- D. IDCT pass 1 (idct_sse2.hpp:102-103): lane (slot, v, v+1) transforms coefficient
             //         rows v, v+1 over u.  Mismatch control (mb_decoder.cpp:150-152; intra DC
@@ -1151,7 +1164,7 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, LT&
             //         lanes with ds_swizzle and applied to QFS[63] (row 7, u 7) before the
             //         transform.  Output transposed in place ([x][v]): the block is read by one
             //         ds_read instruction before any lane writes it.
-            for (int t = lane; t < ((ABL & 1) ? 0 : S.nslots * 4); t += 64) {
+            for (int t = lane; t < (((ABL & 1) || ((ABL & 262144) && odd)) ? 0 : S.nslots * 4); t += 64) {
                 const int slot = t >> 2, v = (t & 3) * 2;
                 short* const bw = (short*)L.blk[wave];
                 lds_uint4_t *pa, *pb;
@@ -1186,7 +1199,7 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, LT&
             // pass 2 (:104-108): lane (slot, x, x+2) transforms columns x, x+2 over v; >>6 -> residual
             // image in the MB's dct_type placement (:166-196); the block area is zeroed for the next
             // group
-            for (int t = lane; t < ((ABL & 1) ? 0 : S.nslots * 4); t += 64) {
+            for (int t = lane; t < (((ABL & 1) || ((ABL & (131072 | 262144)) && odd)) ? 0 : S.nslots * 4); t += 64) {
                 const int slot = t >> 2, xq = t & 3;
                 const int x = (xq & 1) | ((xq & 2) << 1);  // 0, 1, 4, 5
                 short* const bw = (short*)L.blk[wave];
@@ -1333,13 +1346,13 @@ constexpr int kAblCompact = 16 | 32768 | 65536;
 // Occupancy targets per kernel from its LDS: 4:2:0 / 4:2:2 P/B workgroups fit 4 per CU (128
 // VGPRs), 4:4:4 P/B 3 (168 VGPRs cost nothing); the compact I kernels fit 4 (4:4:4) or 6 (80 VGPRs)
 template <int CF, int MCM, int ABL = 0>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MCM == 0 && (ABL & ~kAblCompact) == 0 ? (CF == 3 ? 4 : 6) : (CF == 3 ? 3 : 4)))) void recon_kernel(const mp2vg_picture_t* __restrict__ pics,
+__global__ __launch_bounds__((64 * kernel_waves<MCM, ABL>())) __attribute__((amdgpu_waves_per_eu(MCM == 0 && (ABL & ~kAblCompact) == 0 ? (CF == 3 ? 4 : 6) : (CF == 3 ? 3 : 4)))) void recon_kernel(const mp2vg_picture_t* __restrict__ pics,
                                                     const uint32_t* __restrict__ mbrec,
                                                     const uint32_t* __restrict__ coefs,
                                                     const SliceDesc* __restrict__ slices,
                                                     const Geo geo,
                                                     const uint32_t slice_base, const uint32_t nslices) {
-    using LT = Lds<CF, MCM == 0 && (ABL & ~kAblCompact) == 0>;
+    using LT = Lds<CF, MCM == 0 && (ABL & ~kAblCompact) == 0, kernel_waves<MCM, ABL>()>;
     __shared__ __attribute__((aligned(128))) LT L;  // 128-B aligned: pass1_store
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -1370,7 +1383,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MCM == 0 &&
     c.mbrec = mbrec;
     c.coefs = coefs;
     c.dst_slot = (uint8_t*)geo.ftab[pic->dst_slot];
-    c.wsink = geo.sink + 2048 + ((b * WAVES + wave) & 1023) * 64;
+    c.wsink = geo.sink + 2048 + ((b * LT::NWAVES + wave) & 1023) * 64;
     c.dst_tiles = (uint8_t*)geo.ttab[pic->dst_slot];
     c.dst_rsrc = slot_rsrc(c.dst_slot, (uint32_t)geo.slot_bytes);
     c.tile_rsrc = slot_rsrc(c.dst_tiles, (uint32_t)(2 * geo.slot_bytes));
@@ -1442,7 +1455,7 @@ __global__ void digest_kernel(const uint64_t* __restrict__ ftab, const int32_t* 
 
 template <int CF, int MCM, int ABL>
 static void launch_one(const KArgs& a, const Geo& g, hipStream_t stream) {
-    hipLaunchKernelGGL((recon_kernel<CF, MCM, ABL>), dim3(a.nslices), dim3(256), 0, stream, a.pics,
+    hipLaunchKernelGGL((recon_kernel<CF, MCM, ABL>), dim3(a.nslices), dim3(64 * kernel_waves<MCM, ABL>()), 0, stream, a.pics,
                        (const uint32_t*)a.mbs, a.coefs, a.slices, g, a.slice_base, a.nslices);
 }
 
@@ -1499,6 +1512,8 @@ hipError_t launch_recon(int cf, int mcm, const KArgs& a, hipStream_t stream) {
         case 8192: return launch_mcm<1, 8192>(mcm, a, g, stream);
         case 32768: return launch_mcm<1, 32768>(mcm, a, g, stream);  // no-op: the dev build's own baseline
         case 65536: return launch_mcm<1, 65536>(mcm, a, g, stream);  // tile stores in a 64-KB window
+        case 131072: return launch_mcm<1, 131072>(mcm, a, g, stream);  // pass 2 in every 2nd group only
+        case 262144: return launch_mcm<1, 262144>(mcm, a, g, stream);  // IDCT in every 2nd group only
         default: return hipErrorInvalidValue;
         }
     }
