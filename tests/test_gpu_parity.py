@@ -30,8 +30,10 @@ def test_golden_streams_bit_exact(entry):
     assert got == entry["md5"]
 
 
-def random_batch(width, height, cf, npics, seed, field=True, big=False):
-    """Synthetic record batch exercising every record feature (random MVs kept inside the planes)."""
+def random_batch(width, height, cf, npics, seed, field=True, big=False, n_intra=1):
+    """Synthetic record batch exercising every record feature (random MVs kept inside the planes):
+    pictures 0..n_intra-1 are I, the next one P (forward from the one before), the rest B (forward
+    p-1, backward p-2)."""
     rng = np.random.default_rng(seed)
     mbw, mbh = width // 16, height // 16
     nb = {1: 6, 2: 8, 3: 12}[cf]
@@ -42,9 +44,9 @@ def random_batch(width, height, cf, npics, seed, field=True, big=False):
     cw, ch = (16 if cf == 3 else 8), (8 if cf == 1 else 16)
     for p in range(npics):
         pics[p]["dst_slot"] = p
-        pics[p]["fwd_slot"] = p - 1 if p >= 1 else -1
-        pics[p]["bwd_slot"] = p - 2 if p >= 2 else -1
-        pics[p]["picture_coding_type"] = 1 if p == 0 else (2 if p == 1 else 3)
+        pics[p]["fwd_slot"] = p - 1 if p >= n_intra else -1
+        pics[p]["bwd_slot"] = p - 2 if p >= n_intra + 1 else -1
+        pics[p]["picture_coding_type"] = 1 if p < n_intra else (2 if p == n_intra else 3)
         pics[p]["mb_first"] = p * n
         pics[p]["mb_width"], pics[p]["mb_height"] = mbw, mbh
         pics[p]["alternate_scan"] = rng.integers(0, 2)
@@ -53,13 +55,13 @@ def random_batch(width, height, cf, npics, seed, field=True, big=False):
             m = mbs[p * n + k]
             m["x"], m["y"] = k % mbw, k // mbw
             m["qscale"] = rng.integers(1, 113)
-            intra = p == 0 or rng.random() < 0.1
+            intra = p < n_intra or rng.random() < 0.1
             flags = 0
             if intra:
                 flags |= MB_INTRA
                 cbp = (1 << nb) - 1
             else:
-                d = rng.integers(0, 3) if p >= 2 else 0
+                d = rng.integers(0, 3) if p > n_intra else 0
                 flags |= [MB_FWD, MB_BWD, MB_FWD | MB_BWD][d]
                 fld = field and rng.random() < 0.3
                 if fld:
@@ -180,6 +182,36 @@ def test_anchor_tiles_across_batches(cf):
         ctx.decode()
         ctx.synchronize()
         for p in range(5):
+            got = ctx.download(p)
+            for k in range(3):
+                assert np.array_equal(got[k], exp[p][k]), (p, k)
+
+
+@pytest.mark.parametrize("cf", [1, 2, 3])
+def test_tile_free_i_launch_then_predictions(cf):
+    """A 4:2:0 / 4:2:2 I-only batch in which few pictures store anchor tiles runs the I kernel
+    without its tile store code (launch mode 4) and converts the tiles of the pictures a later
+    batch may read (the last two) right after the launch (runtime.cpp plan_batch / TilePlan); the
+    4:4:4 batch keeps the tile-storing kernel.  Batch 1: 12 I pictures; batch 2: a P picture
+    predicting from picture 11 and B pictures from pictures 11 and 10, read through the tiles;
+    every frame vs the oracle."""
+    w, h = 96, 64
+    pics, mbs, coefs = random_batch(w, h, cf, 16, seed=5150 + cf, n_intra=12)
+    exp = oracle_frames(_P(w, h, cf, pics, mbs, coefs))
+    n = (w // 16) * (h // 16)
+    c0 = int(mbs["coef_off"][12 * n])
+    assert set(R.plan_batch(w, h, cf, 16, pics[:12], mbs[:12 * n], coefs[:c0])[1].tolist()) == {4 if cf < 3 else 0}
+    p2 = pics[12:].copy()
+    p2["mb_first"] -= 12 * n
+    m2 = mbs[12 * n:].copy()
+    m2["coef_off"] -= c0
+    with R.DeviceContext(w, h, cf, slots=16) as ctx:
+        ctx.upload(pics[:12], mbs[:12 * n], coefs[:c0])
+        ctx.decode()
+        ctx.upload(p2, m2, coefs[c0:])
+        ctx.decode()
+        ctx.synchronize()
+        for p in range(16):
             got = ctx.download(p)
             for k in range(3):
                 assert np.array_equal(got[k], exp[p][k]), (p, k)

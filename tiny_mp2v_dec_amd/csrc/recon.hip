@@ -196,7 +196,7 @@ constexpr int G = 4;               // macroblocks per wave group
 #define MP2VG_I_WAVES 4
 #endif
 template <int MCM, int ABL>
-constexpr int kernel_waves() { return MCM == 0 && ABL == 0 ? MP2VG_I_WAVES : WAVES; }
+constexpr int kernel_waves() { return (MCM == 0 || MCM == 4) && ABL == 0 ? MP2VG_I_WAVES : WAVES; }
 
 // Residual image of one MB in LDS (int16): luma 16x16, then Cb CW x CH, then Cr.  Inside each
 // group of 4 pixels the order is x0, x0+2, x0+1, x0+3: one v_perm unpacks the matching
@@ -1018,7 +1018,7 @@ __device__ __forceinline__ void prefetch_words(uint32_t (&cw)[NCW], const SliceC
 //   D, E:      IDCT, add/clip + store of g
 // Every look-ahead value is consumed before its register is reloaded (no loop-carried copies of
 // pending loads), so the waits at the top never cover the previous group's stores.
-template <int CF, int MCM, int ABL, class LT>
+template <int CF, int MCM, int ABL, class LT, bool TILES = true>  // TILES: the anchor-tile store code
 __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, LT& L, int lane, int wave) {
     using F = Fmt<CF>;
     using RL = ResLayout<CF>;
@@ -1308,7 +1308,7 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, LT&
             store_pass_put8<CF, 0, 4>(gr0, glive, lane, geo, c.wsink, c.dst_slot, c.dst_rsrc, res8);
             store_pass_put8<CF, 1, NWC>(gr0, glive, lane, geo, c.wsink, c.dst_slot, c.dst_rsrc, res8);
             if (CF != 1) store_pass_put8<CF, 2, NWC>(gr0, glive, lane, geo, c.wsink, c.dst_slot, c.dst_rsrc, res8);
-            if (c.tiles) {  // MB 0 of the group is always live
+            if (TILES && c.tiles) {  // MB 0 of the group is always live
                 const uint32_t r00 = (uint32_t)__builtin_amdgcn_readfirstlane((int)gr0);
                 tile_group<CF, false, ABL>(r00 & 0xffff, r00 >> 16, lane, geo, c.wsink, c.dst_tiles, c.tile_rsrc, res8);
             }
@@ -1346,13 +1346,16 @@ constexpr int kAblCompact = 16 | 32768 | 65536;
 // Occupancy targets per kernel from its LDS: 4:2:0 / 4:2:2 P/B workgroups fit 4 per CU (128
 // VGPRs), 4:4:4 P/B 3 (168 VGPRs cost nothing); the compact I kernels fit 4 (4:4:4) or 6 (80 VGPRs)
 template <int CF, int MCM, int ABL = 0>
-__global__ __launch_bounds__((64 * kernel_waves<MCM, ABL>())) __attribute__((amdgpu_waves_per_eu(MCM == 0 && (ABL & ~kAblCompact) == 0 ? (CF == 3 ? 4 : 6) : (CF == 3 ? 3 : 4)))) void recon_kernel(const mp2vg_picture_t* __restrict__ pics,
+// MCM: 0 I pictures, 1 P, 2 B, 3 a mixed P/B level (the picture type picks the loop per
+// workgroup), 4 I pictures without the anchor-tile store code (I-only launches where few pictures
+// store tiles: theirs are converted after the launch, runtime.cpp TilePlan)
+__global__ __launch_bounds__((64 * kernel_waves<MCM, ABL>())) __attribute__((amdgpu_waves_per_eu((MCM == 0 || MCM == 4) && (ABL & ~kAblCompact) == 0 ? (CF == 3 ? 4 : 6) : (CF == 3 ? 3 : 4)))) void recon_kernel(const mp2vg_picture_t* __restrict__ pics,
                                                     const uint32_t* __restrict__ mbrec,
                                                     const uint32_t* __restrict__ coefs,
                                                     const SliceDesc* __restrict__ slices,
                                                     const Geo geo,
                                                     const uint32_t slice_base, const uint32_t nslices) {
-    using LT = Lds<CF, MCM == 0 && (ABL & ~kAblCompact) == 0, kernel_waves<MCM, ABL>()>;
+    using LT = Lds<CF, (MCM == 0 || MCM == 4) && (ABL & ~kAblCompact) == 0, kernel_waves<MCM, ABL>()>;
     __shared__ __attribute__((aligned(128))) LT L;  // 128-B aligned: pass1_store
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -1402,7 +1405,9 @@ __global__ __launch_bounds__((64 * kernel_waves<MCM, ABL>())) __attribute__((amd
     c.coef_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)coefs, (short)0, (int)kNoTap, 0x00020000);
     c.mb_begin = sd.mb_begin;
     c.mb_end = sd.mb_begin + sd.mb_count;
-    if constexpr (MCM < 3) {
+    if constexpr (MCM == 4) {
+        run_slice<CF, 0, ABL, LT, false>(c, geo, L, lane, wave);
+    } else if constexpr (MCM < 3) {
         run_slice<CF, (ABL & 2) ? 0 : MCM, ABL, LT>(c, geo, L, lane, wave);
     } else {  // mixed level: the picture type picks the specialised loop (uniform per workgroup)
         const int pct = pic->picture_coding_type;
@@ -1466,6 +1471,7 @@ static hipError_t launch_mcm(int mcm, const KArgs& a, const Geo& g, hipStream_t 
     case 1: launch_one<CF, 1, ABL>(a, g, stream); break;
     case 2: launch_one<CF, 2, ABL>(a, g, stream); break;
     case 3: launch_one<CF, 3, ABL>(a, g, stream); break;
+    case 4: launch_one<CF, 4, ABL>(a, g, stream); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

@@ -32,7 +32,7 @@ struct SliceDesc {
 };
 
 // one kernel launch: a slice range of one dependency level and one motion-compensation mode
-// (0: I pictures, 1: P, forward only, 2: B)
+// (0: I pictures, 1: P, forward only, 2: B, 3: P and B, 4: I pictures without tile stores)
 struct Launch {
     uint32_t begin, end;
     int mcm;

@@ -87,9 +87,10 @@ static int set_coupling() {
 // A reference slot that the batch reads before writing it must hold tiles from an earlier batch;
 // when its tiles are stale (its writer did not store them) mp2vg_batch_decode rebuilds them from
 // the frame (tile_convert) on the reading set's stream first.  The I and P loops store their
-// tiles themselves (building the I pictures' tiles by conversion after their launch instead
-// measured c2 -2.3 %, c1 +2 %); B pictures that a later picture reads (never in an MPEG-2
-// stream) get theirs from tile_convert right after their launch, one launch over its pictures.
+// tiles themselves (building every I picture's tiles by conversion after its launch measured c2
+// -2.3 %), except in I-only launches where few pictures store tiles (mode 4, plan_batch); B
+// pictures that a later picture reads (never in an MPEG-2 stream) and those I pictures get theirs
+// from tile_convert right after their launch, one launch over its pictures.
 struct TilePlan {
     std::vector<std::pair<int32_t, int32_t>> ext_reads;  // (slot, set) read before written
     std::vector<std::pair<int32_t, uint8_t>> writes;     // (slot, tiles written) in decode order
@@ -665,11 +666,25 @@ static int plan_batch(mp2vg_ctx_t* c, const mp2vg_picture_t* pics, int32_t npics
         }
         l.end = (uint32_t)slices.size();
         l.mcm = types == 1 ? 0 : (types == 2 ? 1 : (types == 4 ? 2 : 3));
+        // A 4:2:0 / 4:2:2 I-only launch in which at most a quarter of the pictures store tiles (an
+        // I-only stream: the batch's last two pictures) runs the I kernel without the tile store
+        // code (mode 4: 71 instead of 79 VGPRs, 7 waves per SIMD instead of 6; the 4:4:4 kernel
+        // keeps its 4) and converts those pictures' tiles after it (tile_convert, same stream).
+        // Measured neutral on c1 (one-stream I launch 0.286 ms either way, profiles/r5/README.md):
+        // the skipped stores were already branched over per slice.  (MP2VG_I_TILEFREE=0 in dev
+        // builds keeps mode 0.)
+        static const bool tilefree = !dev_env("MP2VG_I_TILEFREE") || atoi(dev_env("MP2VG_I_TILEFREE")) != 0;
+        int nneed = 0;
+        for (int p : lp) nneed += need[p];
+        if (types == 1 && tilefree && c->g.cf != 3 && nneed * 4 <= (int)lp.size()) {
+            l.mcm = 4;
+            for (uint32_t k = l.begin; k < l.end; k++) slices[k].reserved = 0;
+        }
         l.level = q;
         l.set = set;
         if (tplan)
             for (int p : lp)
-                if (need[p] && pics[p].picture_coding_type == 3)
+                if (need[p] && (pics[p].picture_coding_type == 3 || l.mcm == 4))
                     tplan->post.push_back({(int32_t)launches.size(), pics[p].dst_slot});
         launches.push_back(l);
     }

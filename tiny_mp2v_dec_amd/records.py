@@ -86,7 +86,7 @@ class Parsed:
 def plan_batch(width, height, chroma_format, nslots, pics, mbs, coefs, one_stream=False):
     """mp2vg_batch_validate: the upload's host-side record validation and launch planning, with no
     device.  Returns (launch index of each picture, kernel mode of each launch: 0 I, 1 P, 2 B,
-    3 mixed); raises Mp2vgError for a batch the upload would refuse."""
+    3 mixed, 4 I without tile stores); raises Mp2vgError for a batch the upload would refuse."""
     cfg = _lib.make_config(width, height, chroma_format, pool=nslots,
                            flags=_lib.MP2VG_CTX_ONE_STREAM if one_stream else 0)
     pics = np.ascontiguousarray(pics, PIC_DTYPE)

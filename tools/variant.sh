@@ -8,6 +8,10 @@ OUT=tiny_mp2v_dec_amd/_var/$NAME
 mkdir -p $OUT
 cp tiny_mp2v_dec_amd/_build/*.o $OUT/ 2>/dev/null || true
 hipcc -x hip --offload-arch=gfx950 -munsafe-fp-atomics ${EXTRA:-} -O3 -fPIC -std=c++17 -I tiny_mp2v_dec_amd/csrc -I include -c $SRC -o $OUT/recon.hip.o -Rpass-analysis=kernel-resource-usage 2> $OUT/resource.txt
+# dev builds (EXTRA=-DMP2VG_DEV_ABLATIONS): runtime.cpp's dev_env knobs too
+if [[ "${EXTRA:-}" == *MP2VG_DEV_ABLATIONS* ]]; then
+  hipcc -D__HIP_PLATFORM_AMD__ $EXTRA -w -O3 -fPIC -std=c++17 -I tiny_mp2v_dec_amd/csrc -I include -c tiny_mp2v_dec_amd/csrc/runtime.cpp -o $OUT/runtime.cpp.o
+fi
 hipcc -shared -fPIC --offload-arch=gfx950 -o $OUT/libmp2vg.so $OUT/*.o -lpthread
 python3 - $OUT/resource.txt $NAME <<'PY'
 import re, sys
