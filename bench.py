@@ -396,7 +396,7 @@ def main():
         ms = float(l1[:, sel].mean(axis=0).sum())
         nbytes = float(launch_bytes[sel].sum())
         name = f"recon_kernel<{cf}, {m}, 0>"
-        per_kernel[name] = {"mode": ["I", "P", "B", "P+B", "I, tiles converted after"][m], "launches_per_step": int(sel.sum()),
+        per_kernel[name] = {"mode": ["I", "P / one-direction B", "B", "P+B", "I, tiles converted after"][m], "launches_per_step": int(sel.sum()),
                             "avg_launch_ms": round(ms / int(sel.sum()), 4),
                             "algorithmic_bytes_per_launch": int(nbytes / int(sel.sum())),
                             "achieved_GBps": round(nbytes / (ms / 1e3) / 1e9, 1),

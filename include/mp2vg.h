@@ -160,7 +160,7 @@ int  mp2vg_batch_upload(mp2vg_ctx_t* ctx, const mp2vg_picture_t* pics, int32_t n
  * MP2VG_OK, or MP2VG_E_INVALID with the reason in mp2vg_last_error().  Optional outputs (NULL to
  * skip): *nlaunches = kernel launches per mp2vg_batch_decode; launch_of_pic[npics] = the launch
  * (index into mp2vg_batch_times' launch list) that reconstructs each picture; launch_mode[i <
- * max_launches] = that launch's kernel (0 I, 1 P, 2 B, 3 mixed P/B picture types). */
+ * max_launches] = that launch's kernel (0 I, 1 P, 2 B, 3 mixed P/B picture types, 4 I without tile stores). */
 int  mp2vg_batch_validate(const mp2vg_config_t* cfg, int32_t nslots, const mp2vg_picture_t* pics,
                           int32_t npics, const mp2vg_mb_t* mbs, uint64_t nmbs,
                           const uint32_t* coefs, uint64_t ncoefs, int32_t* nlaunches,

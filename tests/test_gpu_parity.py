@@ -188,6 +188,30 @@ def test_anchor_tiles_across_batches(cf):
 
 
 @pytest.mark.parametrize("cf", [1, 2, 3])
+def test_one_direction_b_pictures_through_the_p_loop(cf):
+    """B pictures that predict in one direction only (a closed GOP's leading B pictures: backward
+    only) run the one-reference P loop with that reference, its vectors and field selects
+    (runtime.cpp plan_batch, recon.hip issue_pass): in a P launch (picture 2, backward only, beside
+    P picture 1) and inside a mixed launch (picture 5, backward only, beside two-direction picture
+    4); picture 3 is forward only.  Every frame vs the oracle."""
+    w, h = 96, 64
+    pics, mbs, coefs = random_batch(w, h, cf, 6, seed=9090 + cf)
+    n = (w // 16) * (h // 16)
+    for p, keep in ((2, MB_BWD), (3, MB_FWD), (5, MB_BWD)):
+        m = mbs[p * n:(p + 1) * n]
+        inter = (m["flags"] & MB_INTRA) == 0
+        m["flags"][inter] = (m["flags"][inter] & np.uint16(0xFFFF & ~(MB_FWD | MB_BWD))) | keep
+    of_pic, modes = R.plan_batch(w, h, cf, 6, pics, mbs, coefs, one_stream=True)
+    assert modes[of_pic[1]] == 1 and of_pic[2] == of_pic[1]  # P + backward-only B: a P launch
+    assert modes[of_pic[5]] == 3 and of_pic[4] == of_pic[5]  # one- and two-direction B: mixed
+    exp = oracle_frames(_P(w, h, cf, pics, mbs, coefs))
+    got = gpu_decode(_P(w, h, cf, pics, mbs, coefs))
+    for p in range(len(pics)):
+        for k in range(3):
+            assert np.array_equal(got[p][k], exp[p][k]), (p, k)
+
+
+@pytest.mark.parametrize("cf", [1, 2, 3])
 def test_tile_free_i_launch_then_predictions(cf):
     """A 4:2:0 / 4:2:2 I-only batch in which few pictures store anchor tiles runs the I kernel
     without its tile store code (launch mode 4) and converts the tiles of the pictures a later

@@ -177,3 +177,16 @@ def test_i_only_launch_modes():
     g = _parsed(1)
     modes = R.plan_batch(g.width, g.height, 1, g.npics, g.pics, g.mbs, g.coefs)[1].tolist()
     assert 0 in modes and 4 not in modes
+
+
+def test_backward_prediction_in_a_p_picture_rejected():
+    """The P loop predicts every non-intra MB of a P picture from the forward reference
+    (recon.hip issue_pass), so a P picture whose MBs predict backward is refused."""
+    p = _parsed(1)
+    k = int(np.nonzero(p.pics["picture_coding_type"] == 2)[0][0])
+    mbs = p.mbs.copy()
+    first = int(p.pics[k]["mb_first"])
+    inter = np.nonzero((mbs["flags"][first:first + 99] & _lib.MB_INTRA) == 0)[0]
+    mbs["flags"][first + inter[0]] |= _lib.MB_BWD
+    with pytest.raises(_lib.Mp2vgError, match="backward prediction in a P picture"):
+        R.validate_batch(p.width, p.height, 1, p.npics, p.pics, mbs, p.coefs)

@@ -497,17 +497,20 @@ __device__ __forceinline__ LaneRec lane_rec(uint32_t rv, int lane) {
     return L;
 }
 
+// MCM 1 (the one-reference loop: P pictures, and B pictures that predict in one direction only,
+// runtime.cpp plan_batch): every non-intra MB predicts from ref_fwd, with its forward (dir 0) or
+// backward (dir 1: ref_fwd then holds the backward reference) vectors and field selects.
 template <int CF, int MCM, int J, int NW, int ABL = 0>
 __device__ __forceinline__ void issue_pass(const LaneRec& L, bool live, int lane, const Geo& geo,
                                            __amdgpu_buffer_rsrc_t ref_fwd, __amdgpu_buffer_rsrc_t ref_bwd,
-                                           Tap<NW>& tf, Tap<NW>& tb) {
+                                           Tap<NW>& tf, Tap<NW>& tb, int dir = 0) {
     using F = Fmt<CF>;
     int k, plane, py;
     pass_row<CF, J>(lane, k, plane, py);
     const uint32_t fl = L.r1 & 0xffff;
     const bool none = !live || (fl & MP2VG_MB_INTRA);
     const bool bwd = fl & MP2VG_MB_BWD;
-    const bool fwd = !none && ((fl & MP2VG_MB_FWD) || !bwd);
+    const bool fwd = !none && (MCM == 1 || (fl & MP2VG_MB_FWD) || !bwd);
     const bool field = fl & MP2VG_MB_FIELD_MC;
     const int pw = plane == 0 ? 16 : F::CW;
     const int phm = plane == 0 ? 16 : F::CH;
@@ -518,8 +521,9 @@ __device__ __forceinline__ void issue_pass(const LaneRec& L, bool live, int lane
     const int ph = gsel(geo.ph, plane);
     constexpr bool TL = J == 0 || kChromaTiles;
     const uint32_t off = (TL ? 2u : 1u) * (uint32_t)gsel(geo.plane_off, plane);  // the plane in the tile slot
-    tap_issue<CF, NW, ABL, TL>(tf, fwd, ref_fwd, off, L.mvf, plane, gx, py, phm, mbyb, field, (fl >> (8 + 2 * r)) & 1,
-                               stride, ph);
+    const uint32_t mv1 = (MCM == 1 && dir) ? L.mvb : L.mvf;
+    const int fsh = 8 + 2 * r + (MCM == 1 ? dir : 0);
+    tap_issue<CF, NW, ABL, TL>(tf, fwd, ref_fwd, off, mv1, plane, gx, py, phm, mbyb, field, (fl >> fsh) & 1, stride, ph);
     if (MCM == 2)
         tap_issue<CF, NW, ABL, TL>(tb, !none && bwd, ref_bwd, off, L.mvb, plane, gx, py, phm, mbyb, field,
                                    (fl >> (9 + 2 * r)) & 1, stride, ph);
@@ -865,6 +869,7 @@ struct SliceCtx {
     uint8_t* dst_tiles;  // the picture's anchor tiles
     __amdgpu_buffer_rsrc_t dst_rsrc, tile_rsrc;  // the same as buffer resources (store policies)
     bool tiles;          // ... which it writes (SliceDesc.reserved bit 0, runtime.cpp TilePlan)
+    int dir;             // MCM 1: 1 = the one reference is the backward one (SliceDesc.reserved bit 2)
     // this wave's own 64-B sink line (dummy and dead-lane stores): stores of many waves to one
     // address serialize in one L2 channel, and a wave's first loop-head wait covers its own
     uint8_t* wsink;
@@ -1048,7 +1053,7 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, LT&
         const int ng = (int)min(mb_end - g, (uint32_t)G);
         glive = kl < ng;
         const LaneRec R = lane_rec(rv, lane);
-        if (MCM) issue_pass<CF, MCM, 0, 4, ABL>(R, glive, lane, geo, c.ref_fwd, c.ref_bwd, t0f, t0b);
+        if (MCM) issue_pass<CF, MCM, 0, 4, ABL>(R, glive, lane, geo, c.ref_fwd, c.ref_bwd, t0f, t0b, c.dir);
         S = group_state<NB>(rv, ng);
         gr0 = R.r0;
         gr1 = R.r1;
@@ -1057,8 +1062,8 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, LT&
         prefetch_words<MCM, NCW>(cw, c, S.coef0, S.ncoef, lane);
         __builtin_amdgcn_sched_barrier(0);
         if (MCM) {
-            issue_pass<CF, MCM, 1, NWC, ABL>(R, glive, lane, geo, c.cref_fwd, c.cref_bwd, t1f, t1b);
-            if (CF != 1) issue_pass<CF, MCM, 2, NWC, ABL>(R, glive, lane, geo, c.cref_fwd, c.cref_bwd, t2f, t2b);
+            issue_pass<CF, MCM, 1, NWC, ABL>(R, glive, lane, geo, c.cref_fwd, c.cref_bwd, t1f, t1b, c.dir);
+            if (CF != 1) issue_pass<CF, MCM, 2, NWC, ABL>(R, glive, lane, geo, c.cref_fwd, c.cref_bwd, t2f, t2b, c.dir);
         }
         __builtin_amdgcn_sched_barrier(0);
         // the steady-state loop issues the group's stores after these loads: dummy stores to the
@@ -1096,7 +1101,7 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, LT&
         const int ngN = (int)min(mb_end - gn, (uint32_t)G);
         const bool gliveN = kl < ngN;
         const LaneRec R = lane_rec(rvN, lane);
-        if (MCM) issue_pass<CF, MCM, 0, 4, ABL>(R, gliveN, lane, geo, c.ref_fwd, c.ref_bwd, t0f, t0b);
+        if (MCM) issue_pass<CF, MCM, 0, 4, ABL>(R, gliveN, lane, geo, c.ref_fwd, c.ref_bwd, t0f, t0b, c.dir);
         const Group SN = group_state<NB>(rvN, ngN);
         __builtin_amdgcn_sched_barrier(0);
         rvN = rec_load(c.mbrec, g + 2 * STEP < mb_end ? g + 2 * STEP : g, mb_last, lane);
@@ -1191,8 +1196,8 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, LT&
             // chroma taps of g+1 issued mid-iteration: spreads the wave's TA demand
             __builtin_amdgcn_sched_barrier(0);
             if (MCM) {
-                issue_pass<CF, MCM, 1, NWC, ABL>(R, gliveN, lane, geo, c.cref_fwd, c.cref_bwd, t1f, t1b);
-                if (CF != 1) issue_pass<CF, MCM, 2, NWC, ABL>(R, gliveN, lane, geo, c.cref_fwd, c.cref_bwd, t2f, t2b);
+                issue_pass<CF, MCM, 1, NWC, ABL>(R, gliveN, lane, geo, c.cref_fwd, c.cref_bwd, t1f, t1b, c.dir);
+                if (CF != 1) issue_pass<CF, MCM, 2, NWC, ABL>(R, gliveN, lane, geo, c.cref_fwd, c.cref_bwd, t2f, t2b, c.dir);
             }
             __builtin_amdgcn_sched_barrier(0);
             stamp<ABL>(st, 3);
@@ -1391,9 +1396,14 @@ __global__ __launch_bounds__((64 * kernel_waves<MCM, ABL>())) __attribute__((amd
     c.dst_rsrc = slot_rsrc(c.dst_slot, (uint32_t)geo.slot_bytes);
     c.tile_rsrc = slot_rsrc(c.dst_tiles, (uint32_t)(2 * geo.slot_bytes));
     c.tiles = sd.reserved & 1u;
+    // SliceDesc.reserved bit 1: a B picture that predicts in one direction only, run by the
+    // one-reference loop (MCM 1); bit 2: that direction is backward (runtime.cpp plan_batch)
+    const bool one_dir = sd.reserved & 2u;
+    c.dir = (sd.reserved >> 2) & 1u;
     // the taps read the references' anchor tiles (tile slot = 2 x slot bytes)
-    const int fs = pic->fwd_slot < 0 ? pic->dst_slot : pic->fwd_slot;
+    const int fs0 = pic->fwd_slot < 0 ? pic->dst_slot : pic->fwd_slot;
     const int bs = pic->bwd_slot < 0 ? pic->dst_slot : pic->bwd_slot;
+    const int fs = c.dir ? bs : fs0;
     c.ref_fwd = slot_rsrc((const uint8_t*)geo.ttab[fs], (uint32_t)(2 * geo.slot_bytes));
     c.ref_bwd = slot_rsrc((const uint8_t*)geo.ttab[bs], (uint32_t)(2 * geo.slot_bytes));
     if (kChromaTiles) {
@@ -1411,9 +1421,9 @@ __global__ __launch_bounds__((64 * kernel_waves<MCM, ABL>())) __attribute__((amd
         run_slice<CF, (ABL & 2) ? 0 : MCM, ABL, LT>(c, geo, L, lane, wave);
     } else {  // mixed level: the picture type picks the specialised loop (uniform per workgroup)
         const int pct = pic->picture_coding_type;
-        if (pct == 3)
+        if (pct == 3 && !one_dir)
             run_slice<CF, (ABL & 2) ? 0 : 2, ABL, LT>(c, geo, L, lane, wave);
-        else if (pct == 2)
+        else if (pct == 2 || one_dir)
             run_slice<CF, (ABL & 2) ? 0 : 1, ABL, LT>(c, geo, L, lane, wave);
         else
             run_slice<CF, 0, ABL, LT>(c, geo, L, lane, wave);

@@ -520,6 +520,11 @@ static int plan_batch(mp2vg_ctx_t* c, const mp2vg_picture_t* pics, int32_t npics
             return MP2VG_E_INVALID;
         }
         const bool uses[2] = {uses_of[2 * (size_t)p] != 0, uses_of[2 * (size_t)p + 1] != 0};
+        // the P loop predicts every non-intra MB from the forward reference (recon.hip issue_pass)
+        if (P.picture_coding_type == 2 && uses[1]) {
+            set_error("backward prediction in a P picture");
+            return MP2VG_E_INVALID;
+        }
         if ((uses[0] && P.fwd_slot < 0) || (uses[1] && P.bwd_slot < 0)) {
             set_error("picture predicts from a missing reference slot");
             return MP2VG_E_INVALID;
@@ -637,16 +642,32 @@ static int plan_batch(mp2vg_ctx_t* c, const mp2vg_picture_t* pics, int32_t npics
         if (lp.empty()) continue;
         Launch l;
         l.begin = (uint32_t)slices.size();
+        // B pictures that predict in one direction only (a closed GOP's leading B pictures:
+        // backward only) run the one-reference P loop with that reference (SliceDesc.reserved
+        // bits 1-2, recon.hip issue_pass): a launch of P and such B pictures is a P launch
+        // (MP2VG_ONE_DIR_B=0 in dev builds: every B picture in the B loop)
+        static const bool route = !dev_env("MP2VG_ONE_DIR_B") || atoi(dev_env("MP2VG_ONE_DIR_B")) != 0;
+        auto one_dir = [&](int p) {
+            return route && pics[p].picture_coding_type == 3 && !(uses_of[2 * (size_t)p] && uses_of[2 * (size_t)p + 1]);
+        };
         int types = 0;
         for (int p : lp) {
             const int pct = pics[p].picture_coding_type;
-            types |= 1 << (pct == 1 ? 0 : (pct == 2 ? 1 : 2));
+            types |= 1 << (pct == 1 ? 0 : (pct == 2 || one_dir(p) ? 1 : 2));
         }
         // Pictures that read a common reference slot (the two B pictures between a pair of
         // anchors and the P picture after them) form a cluster whose slices are interleaved row
         // by row, so their workgroups read the same reference lines at about the same time on
         // the same XCD (measured: +0.6 % on c2).
         auto reads = [&](int p, int s) { return s >= 0 && (pics[p].fwd_slot == s || pics[p].bwd_slot == s); };
+        // bit 0: the picture stores its anchor tiles in the loop (I and P; B pictures read later
+        // get theirs from tile_convert after the launch, TilePlan.post); bit 1: one-direction B
+        // picture (P loop); bit 2: its one direction is backward
+        auto sflags = [&](int p) -> uint32_t {
+            const bool b = pics[p].picture_coding_type == 3;
+            const bool bwd_only = !uses_of[2 * (size_t)p] && uses_of[2 * (size_t)p + 1];
+            return (uint32_t)(need[p] && !b) | (one_dir(p) ? 2u : 0u) | (one_dir(p) && bwd_only ? 4u : 0u);
+        };
         size_t i = 0;
         while (i < lp.size()) {
             size_t j = i + 1;
@@ -661,7 +682,7 @@ static int plan_batch(mp2vg_ctx_t* c, const mp2vg_picture_t* pics, int32_t npics
             for (int r = 0; r < mbh; r += slice_rows)
                 for (size_t k = i; k < j; k++)
                     slices.push_back({(uint32_t)lp[k], pics[lp[k]].mb_first + (uint32_t)(r * mbw),
-                                      (uint32_t)(std::min(slice_rows, mbh - r) * mbw), need[lp[k]]});
+                                      (uint32_t)(std::min(slice_rows, mbh - r) * mbw), sflags(lp[k])});
             i = j;
         }
         l.end = (uint32_t)slices.size();

@@ -56,7 +56,7 @@ def main():
         n = int(sel.sum())
         nbytes = float(launch_bytes[sel].sum())
         out["per_kernel"][f"recon_kernel<{cf}, {m}, 0>"] = {
-            "mode": ["I", "P", "B", "P+B", "I, tiles converted after"][m], "launches_per_batch": n, "avg_launch_ms": round(ms / n, 4),
+            "mode": ["I", "P / one-direction B", "B", "P+B", "I, tiles converted after"][m], "launches_per_batch": n, "avg_launch_ms": round(ms / n, 4),
             "algorithmic_bytes_per_launch": int(nbytes / n),
             "frac": round(nbytes / (ms / 1e3) / 1e9 / bench.HBM_PEAK_GBS, 4)}
     print(json.dumps(out), flush=True)
