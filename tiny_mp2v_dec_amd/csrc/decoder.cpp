@@ -340,13 +340,15 @@ extern "C" int mp2vg_decoder_frames_allocated(const mp2vg_decoder_t* d) {
 extern "C" int mp2vg_decoder_decode(mp2vg_decoder_t* d, const uint8_t* buf, uint64_t len) {
     if (!d || !buf) return MP2VG_E_INVALID;
     // the parse runs on worker threads while the chunks below go through the device: a chunk
-    // waits only for its own pictures (two threads are left for this loop and the renderer)
+    // waits only for its own pictures (one thread is left for this loop; the renderer mostly
+    // waits on downloads)
     double t0 = now_ms(), tc;
     double t_up = 0, t_dec = 0, t_down = 0, t_wait = 0, t_gather = 0;
     ParseSession* ps = nullptr;
     const int threads = d->cfg.num_threads > 0 ? d->cfg.num_threads : (int)std::thread::hardware_concurrency();
-    // (16-thread box: 2 or 4 threads kept back 1,975 frames/s, 1 -> 1,864, 6 -> 1,661)
-    int rc = parse_session_start(buf, len, &d->cfg, std::max(1, threads - 2), 4 * kChunk, &ps);
+    // (c2 stream, 768 frames, the GPU box's 16-CPU share, profiles/r5/dropin_threads.jsonl: 2 threads
+    // kept back 8.9-9.3k frames/s, 1 -> 9.7-9.9k, 0 -> 9.6-10.0k, 16 workers on 18 threads 9.4-9.6k)
+    int rc = parse_session_start(buf, len, &d->cfg, std::max(1, threads - 1), 4 * kChunk, &ps);
     t0 = trace_phase("dropin: headers", t0);
     if (rc != MP2VG_OK) return rc;
     std::unique_ptr<ParseSession, void (*)(ParseSession*)> guard(ps, parse_session_free);
