@@ -484,7 +484,7 @@ def e2e_dropin(es, width, height, cf, frames, device, cpu, device_frames=False):
     """The drop-in API end to end on the same stream: mp2v_decoder_c(config, renderer).decode(buf)
     with host frame_c frames (parse, upload, decode, D2H, display-order render callbacks), i.e.
     what a caller of the reference API sees (reference tiny_mp2v_dec.cpp:50-55 times decode()
-    the same way).  PCIe-inclusive: never the bench `value`.  device_frames: the opt-in
+    the same way); best of two decode() calls on one decoder, like cpu_baseline's best of 2.  PCIe-inclusive: never the bench `value`.  device_frames: the opt-in
     MP2VG_DECODER_DEVICE_FRAMES path (frames handed to the renderer in HBM, no D2H)."""
     from tiny_mp2v_dec_amd.decoder import decoder_config_t, mp2v_decoder_c
     share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 2)
@@ -496,15 +496,20 @@ def e2e_dropin(es, width, height, cf, frames, device, cpu, device_frames=False):
 
     dec = mp2v_decoder_c(decoder_config_t(width, height, cf, pictures_pool_size=24, num_threads=threads,
                                           device=device, device_frames=device_frames), render)
+    runs = []
     try:
-        t = time.perf_counter()
-        dec.decode(es, len(es))
-        dt = time.perf_counter() - t
+        for _ in range(2):  # best of 2, as cpu_baseline's reference runs (the host is shared)
+            count[0] = 0
+            t = time.perf_counter()
+            dec.decode(es, len(es))
+            runs.append(time.perf_counter() - t)
+            if count[0] != frames:
+                raise RuntimeError(f"drop-in rendered {count[0]} of {frames} frames")
     finally:
         dec.close()
-    if count[0] != frames:
-        raise RuntimeError(f"drop-in rendered {count[0]} of {frames} frames")
+    dt = min(runs)
     out = {"value": round(frames / dt, 1), "unit": "frames/s", "host_threads": threads, "frames": frames,
+           "runs_frames_per_s": [round(frames / r, 1) for r in runs],
            "scope": "drop-in mp2v_decoder_c::decode() on the bench stream: host parse + record upload + "
                     + ("GPU reconstruct into device frame_c (HBM, no D2H) + render callbacks" if device_frames else
                        "GPU reconstruct + D2H into host frame_c + render callbacks")}
