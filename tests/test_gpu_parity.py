@@ -147,8 +147,9 @@ class _P:  # minimal Parsed-like holder for oracle_frames
 @pytest.mark.parametrize("size", [(96, 64), (128, 48)], ids=["6mb_rows", "8mb_rows"])
 def test_random_records_vs_oracle(cf, big, size):
     """Synthetic record batches (all MB kinds, field MC / DCT, saturating levels) vs the oracle.
-    8-MB rows (a multiple of the kernel's 4-MB group): the P/B launches' workgroups take two MB
-    rows each (runtime.cpp plan_batch), three rows leave a one-row last slice."""
+    8-MB rows (a multiple of the kernel's 4-MB group): the P/B launches' workgroups take two
+    one-row slices each (runtime.cpp plan_batch `mates`); a launch of one picture's three rows
+    leaves a workgroup with one slice."""
     w, h = size
     pics, mbs, coefs = random_batch(w, h, cf, 5, seed=1729 + cf + 10 * big, big=big)
     exp = oracle_frames(_P(w, h, cf, pics, mbs, coefs))

@@ -2,7 +2,8 @@
 // packed 16-bit VALU, v_lerp_u8, LDS per wave; no CUDA-compat layer).  See recon_kernel.h for
 // the map to the reference.
 //
-// Work decomposition: one workgroup (4 waves) per slice (= MB row, XCD-aware order); each wave
+// Work decomposition: one workgroup (4 waves) per slice (= MB row, XCD-aware order), or in P/B
+// launches two slices of reference-sharing pictures, two waves each (`mates`); each wave
 // reconstructs groups of G = 4 consecutive macroblocks with wave-private LDS:
 //   A  group records (scalar loads) + first 64 coefficient words
 //   B  reference-row loads for every pixel row of the group (one lane per row: 16-px luma rows,
@@ -786,13 +787,15 @@ struct Lds {
     short res[NWV][C8 ? G * ResLayout<CF>::SIZE / 2 : G * ResLayout<CF>::SIZE];
     uint8_t map[NWV][MAXS];                      // slot -> k*16 + b
     uint32_t dq[NWV][64];                        // (k*16 + b) -> dequant parameters (DqEntry)
-    uint8_t W[4][64];
+    // quantiser matrices and scan (C8: the I kernels' one picture per workgroup; P/B layouts two
+    // sets, one per half of the workgroup when it runs two slices, recon_kernel `mates`)
+    uint8_t W[C8 ? 4 : 8][64];
     // I kernels (WB): the intra matrix row of each block b (W[0] for b < 6, W[2] above), so a
     // coefficient word's (b, i) bits 16-25 index it directly; scan positions stored doubled (byte
     // offsets of an int16 in the block).  The table sits after `scan`: c5 is sensitive to where
     // the small tables sit (scan 64 B further on: -5 %; the table in front of scan: -1 %)
     static constexpr bool WB = C8;
-    uint8_t scan[64];
+    uint8_t scan[C8 ? 64 : 128];
     uint8_t Wb[WB && CF != 1 ? Fmt<CF>::NB : 0][64];  // zero-length (clang extension) when unused: no layout change
     // short index of coefficient / pass-1 output idx (0..63) of a slot, relative to the wave's blk
     __device__ static int bofs(int slot, int idx) { return slot * BLK + (C8 ? (idx ^ ((slot & 7) << 3)) : idx); }
@@ -877,6 +880,10 @@ struct SliceCtx {
     __amdgpu_buffer_rsrc_t cref_fwd, cref_bwd;  // chroma taps' source (the tiles, or frame rows)
     __amdgpu_buffer_rsrc_t coef_rsrc;  // the batch's words; offsets >= kNoTap read nothing
     uint32_t mb_begin, mb_end;
+    // the wave's place among the waves of its slice and their group stride (STEP MBs): 4 waves
+    // per slice, or 2 when the workgroup runs two slices (recon_kernel `mates`, half 0 / 1)
+    uint32_t wpos, step;
+    int half;
 };
 
 // Per-group dequant parameters of block b of MB k, built once per group by lane k*16 + b:
@@ -906,7 +913,7 @@ __device__ __forceinline__ int mul24i_asm(int a, int b) {  // v_mul_i32_i24: sig
 // coefficients) needs no table: the slot is k * NB + b, the matrix is the block's (luma for
 // blocks 0-5, mb_decoder.cpp:111-113), the quantiser scale is byte k of qs8.
 template <class LT, bool INTRA_ONLY = false, int NB = 6>
-__device__ __forceinline__ void dequant_word(LT& L, int wave, uint32_t w, uint32_t qs8, bool live = true) {
+__device__ __forceinline__ void dequant_word(LT& L, int wave, uint32_t w, uint32_t qs8, bool live = true, int h = 0) {
     if constexpr (INTRA_ONLY) {
         const uint32_t k = (w >> 26) & 3u, b = (w >> 22) & 15u;
         const int slot = (int)(k * NB + b);
@@ -914,8 +921,8 @@ __device__ __forceinline__ void dequant_word(LT& L, int wave, uint32_t w, uint32
         const int level = (short)(w & 0xffff);
         // 4:2:0: every block uses the luma intra matrix (blocks 4/5 too, mb_decoder.cpp:184-185),
         // so W[0][i] directly: one 64-B table, no bank conflicts between block rows
-        const int Wi = NB == 6 ? L.W[0][i]
-                               : (LT::WB ? ((const uint8_t*)L.Wb)[(w >> 16) & 0x3ffu] : L.W[b < 6 ? 0 : 2][i]);
+        const int Wi = NB == 6 ? L.W[4 * h][i]
+                               : (LT::WB ? ((const uint8_t*)L.Wb)[(w >> 16) & 0x3ffu] : L.W[4 * h + (b < 6 ? 0 : 2)][i]);
         const uint32_t wq = __umul24((uint32_t)Wi, pick8(qs8, (int)k));
         // (|level| * W * qs) >> 4 with the sign applied after the shift (truncation toward zero):
         // the signed product, biased by 15 when negative, then an arithmetic shift
@@ -934,11 +941,11 @@ __device__ __forceinline__ void dequant_word(LT& L, int wave, uint32_t w, uint32
         if constexpr (LT::WB) {
             // byte address: slot * 128 + ((slot & 7) * 16 XOR doubled scan position)
             const uint32_t a = (uint32_t)(uintptr_t)(lds_short2_t*)L.blk[wave] + ((uint32_t)slot << 7) +
-                               ((((uint32_t)slot << 4) & 0x70u) ^ (uint32_t)L.scan[i]);
+                               ((((uint32_t)slot << 4) & 0x70u) ^ (uint32_t)L.scan[64 * h + i]);
             const uint32_t d = (uint32_t)(uintptr_t)(lds_short2_t*)L.res[wave];
             *(__attribute__((address_space(3))) short*)(uintptr_t)(live ? a : d) = o;
         } else {
-            short* const dst = live ? &((short*)L.blk[wave])[LT::bofs(slot, L.scan[i])] : (short*)L.res[wave];
+            short* const dst = live ? &((short*)L.blk[wave])[LT::bofs(slot, L.scan[64 * h + i])] : (short*)L.res[wave];
             *dst = o;
         }
         return;
@@ -955,7 +962,7 @@ __device__ __forceinline__ void dequant_word(LT& L, int wave, uint32_t w, uint32
     const int level = (short)(w & 0xffff);
     const bool dc = w & MP2VG_COEF_DC;  // QFS[0] = dc << (3 - prec), outside the parity sum (:160)
     const bool s1 = !INTRA_ONLY && (w & MP2VG_COEF_FIRST1S);
-    const int Wi = L.W[(e >> 16) & 3][i];
+    const int Wi = L.W[4 * h + ((e >> 16) & 3)][i];
     const int sign = level < 0 ? -1 : 0;
     const int mag = level < 0 ? -level : level;
     // W*qs < 2^16 and 2*|level|+1 <= 65537 < 2^24: 24-bit multiplies (full rate) give the low 32
@@ -970,7 +977,7 @@ __device__ __forceinline__ void dequant_word(LT& L, int wave, uint32_t w, uint32
         v = s1 ? (short)((t1 ^ sign) - sign) : v;
     }
     v = dc ? (short)level : v;  // branch-free: every lane of the word round writes once
-    ((short*)L.blk[wave])[LT::bofs(slot, L.scan[i])] = v;  // i = 0 for DC and '1s' words: block position 0
+    ((short*)L.blk[wave])[LT::bofs(slot, L.scan[64 * h + i])] = v;  // i = 0 for DC and '1s' words: block position 0
 }
 
 // force the wait for every tap load here (an empty asm reading the registers): a direction
@@ -1028,12 +1035,12 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, LT&
     using F = Fmt<CF>;
     using RL = ResLayout<CF>;
     constexpr int NB = F::NB;
-    constexpr int STEP = LT::STEP;
+    const uint32_t STEP = c.step;
     constexpr int NWC = F::CW / 4;
     // 4:2:0 intra groups (24 blocks) run both IDCT passes in shared rounds (D' below)
     constexpr bool UNI = LT::COMPACT && CF == 1;
     const uint32_t mb_end = c.mb_end, mb_last = c.mb_end - 1;
-    uint32_t g = c.mb_begin + wave * G;
+    uint32_t g = c.mb_begin + c.wpos * G;
     if (g >= mb_end) return;
     const int kl = lane & 3;
 
@@ -1122,12 +1129,12 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, LT&
 #pragma unroll
                 for (int j = 0; j < NCW; j++) {
                     if (64 * j >= S.ncoef) break;
-                    dequant_word<LT, true, NB>(L, wave, cw[j], S.qs8, 64 * j + lane < S.ncoef);
+                    dequant_word<LT, true, NB>(L, wave, cw[j], S.qs8, 64 * j + lane < S.ncoef, c.half);
                 }
             } else {
 #pragma unroll
                 for (int j = 0; j < NCW; j++)
-                    if (64 * j + lane < S.ncoef) dequant_word<LT, false, NB>(L, wave, cw[j], S.qs8);
+                    if (64 * j + lane < S.ncoef) dequant_word<LT, false, NB>(L, wave, cw[j], S.qs8, true, c.half);
             }
             // words past the prefetch: XW loads per lane in flight per round trip, not one (a 4:4:4
             // intra group carries ~1,400 words)
@@ -1142,7 +1149,7 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, LT&
                     }
 #pragma unroll
                     for (int j = 0; j < XW; j++)
-                        if (base + 64 * j + lane < S.ncoef) dequant_word<LT, MCM == 0, NB>(L, wave, xw[j], S.qs8);
+                        if (base + 64 * j + lane < S.ncoef) dequant_word<LT, MCM == 0, NB>(L, wave, xw[j], S.qs8, true, c.half);
                 }
                 // Drain this rare path's loads before it rejoins: the waitcnt pass merges the
                 // paths' pending-load state, and a load it cannot prove retired (a lane-masked
@@ -1359,33 +1366,44 @@ __global__ __launch_bounds__((64 * kernel_waves<MCM, ABL>())) __attribute__((amd
                                                     const uint32_t* __restrict__ coefs,
                                                     const SliceDesc* __restrict__ slices,
                                                     const Geo geo,
-                                                    const uint32_t slice_base, const uint32_t nslices) {
+                                                    const uint32_t slice_base, const uint32_t nslices,
+                                                    const uint32_t mates) {
     using LT = Lds<CF, (MCM == 0 || MCM == 4) && (ABL & ~kAblCompact) == 0, kernel_waves<MCM, ABL>()>;
     __shared__ __attribute__((aligned(128))) LT L;  // 128-B aligned: pass1_store
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    // XCD-aware bijection: XCD x = b % 8 owns the contiguous slice range [x*q + min(x, r), ...)
-    const uint32_t b = blockIdx.x, q8 = nslices / 8, r8 = nslices % 8, xcd = b % 8;
-    const uint32_t si = xcd * q8 + min(xcd, r8) + b / 8;
-    const SliceDesc sd = slices[slice_base + si];
+    // Work units: one slice, or with `mates` (P/B launches, runtime.cpp plan_batch) two
+    // consecutive slices -- cluster mates, the same MB row of two pictures that read the same
+    // references -- waves 0-1 on the first, 2-3 on the second.  XCD-aware bijection: XCD x = b % 8
+    // owns the contiguous unit range [x*q + min(x, r), ...)
+    constexpr bool MATES_OK = !LT::COMPACT && LT::NWAVES == 4;
+    const bool two = MATES_OK && mates != 0;
+    const uint32_t nunits = two ? (nslices + 1) / 2 : nslices;
+    const uint32_t b = blockIdx.x, q8 = nunits / 8, r8 = nunits % 8, xcd = b % 8;
+    const uint32_t unit = xcd * q8 + min(xcd, r8) + b / 8;
+    const int half = two ? (wave >> 1) : 0;
+    const uint32_t si = two ? 2 * unit + (uint32_t)half : unit;
+    const bool have = si < nslices;  // (the last unit of an odd count has one slice)
+    const SliceDesc sd = slices[slice_base + (have ? si : si - 1)];
     const mp2vg_picture_t* pic = pics + sd.pic;
     const int alt = pic->alternate_scan & 1;
 
-    if (tid < 64) {
-        ((uint32_t*)L.W)[tid] = ((const uint32_t*)pic->W)[tid];
+    if ((two ? (tid & 127) : tid) < 64) {
+        ((uint32_t*)L.W)[64 * half + lane] = ((const uint32_t*)pic->W)[lane];
         // blocks sit in LDS pair-interleaved: coefficient (v, u) at (v >> 1) * 16 + u * 2 + (v & 1),
         // so a dword is the (row v, row v + 1) pair of column u that IDCT pass 1 transforms
-        const int r = c_scan_raster[alt][tid];
+        const int r = c_scan_raster[alt][lane];
         const int pos = (r >> 4) * 16 + (r & 7) * 2 + ((r >> 3) & 1);
-        L.scan[tid] = (uint8_t)(LT::WB ? 2 * pos : pos);
+        L.scan[64 * half + lane] = (uint8_t)(LT::WB ? 2 * pos : pos);
         if constexpr (LT::WB && CF != 1) {
 #pragma unroll
-            for (int bb = 0; bb < Fmt<CF>::NB; bb++) L.Wb[bb][tid] = pic->W[bb < 6 ? 0 : 2][tid];
+            for (int bb = 0; bb < Fmt<CF>::NB; bb++) L.Wb[bb][lane] = pic->W[bb < 6 ? 0 : 2][lane];
         }
     }
     for (int i = lane; i < LT::MAXS * LT::BLK / 2; i += 64) ((uint32_t*)L.blk[wave])[i] = 0;
     __syncthreads();
+    if (!have) return;
 
     SliceCtx c;
     c.mbrec = mbrec;
@@ -1415,6 +1433,9 @@ __global__ __launch_bounds__((64 * kernel_waves<MCM, ABL>())) __attribute__((amd
     c.coef_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)coefs, (short)0, (int)kNoTap, 0x00020000);
     c.mb_begin = sd.mb_begin;
     c.mb_end = sd.mb_begin + sd.mb_count;
+    c.half = half;
+    c.wpos = two ? (uint32_t)(wave & 1) : (uint32_t)wave;
+    c.step = (two ? 2u : (uint32_t)LT::NWAVES) * G;
     if constexpr (MCM == 4) {
         run_slice<CF, 0, ABL, LT, false>(c, geo, L, lane, wave);
     } else if constexpr (MCM < 3) {
@@ -1470,8 +1491,10 @@ __global__ void digest_kernel(const uint64_t* __restrict__ ftab, const int32_t* 
 
 template <int CF, int MCM, int ABL>
 static void launch_one(const KArgs& a, const Geo& g, hipStream_t stream) {
-    hipLaunchKernelGGL((recon_kernel<CF, MCM, ABL>), dim3(a.nslices), dim3(64 * kernel_waves<MCM, ABL>()), 0, stream, a.pics,
-                       (const uint32_t*)a.mbs, a.coefs, a.slices, g, a.slice_base, a.nslices);
+    const bool two = a.mates && MCM != 0 && MCM != 4 && kernel_waves<MCM, ABL>() == 4;
+    hipLaunchKernelGGL((recon_kernel<CF, MCM, ABL>), dim3(two ? (a.nslices + 1) / 2 : a.nslices),
+                       dim3(64 * kernel_waves<MCM, ABL>()), 0, stream, a.pics, (const uint32_t*)a.mbs, a.coefs,
+                       a.slices, g, a.slice_base, a.nslices, two ? 1u : 0u);
 }
 
 template <int CF, int ABL>

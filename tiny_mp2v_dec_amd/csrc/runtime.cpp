@@ -625,14 +625,19 @@ static int plan_batch(mp2vg_ctx_t* c, const mp2vg_picture_t* pics, int32_t npics
     }
     slices.clear();
     launches.clear();
-    // MB rows per workgroup (the kernel's "slice"): 2 in launches with P/B pictures, 1 in I-only
-    // launches.  A 1080p row is 30 four-MB groups, 8/8/7/7 over a workgroup's four waves, so two
-    // of them idle for the row's last iteration; two rows are 15 groups per wave, and half as many
-    // pipeline ramps.  Measured (c2, same box, 2 rounds, profiles/r5/README.md): 2 rows +2.4 %
-    // (355.4k -> 363.9k frames/s), 3 rows +1.6 %; the I kernel prefers 1 row (c1 -2 % with 2).
-    // Groups never straddle rows when the row is a multiple of 4 MBs; other widths keep 1 row.
-    // (MP2VG_SLICE_ROWS / MP2VG_SLICE_ROWS_I override in dev builds.)
+    // MB rows per slice: 1 (two slices per workgroup in P/B launches, `mates` below; before them
+    // P/B workgroups took two rows of one picture: a 1080p row is 30 four-MB groups, 8/8/7/7 over
+    // a workgroup's four waves, and two rows made it 15 per wave, +2.4 % over one row).  Groups
+    // never straddle rows when the row is a multiple of 4 MBs; other widths keep 1 row and no
+    // mates.  (MP2VG_SLICE_ROWS / MP2VG_SLICE_ROWS_I override in dev builds.)
     static const int rows_pb = dev_env("MP2VG_SLICE_ROWS") ? std::max(1, atoi(dev_env("MP2VG_SLICE_ROWS"))) : 2;
+    // P/B launches run one-row slices, two per workgroup (`mates`, recon.hip recon_kernel): the
+    // consecutive slices of a reference-sharing cluster, i.e. the same MB row of two pictures that
+    // read the same anchors, waves 0-1 on one and 2-3 on the other.  Same balance as two rows of
+    // one picture (15 groups per wave), half the MB rows in flight per XCD, and both pictures'
+    // taps of one anchor region on one CU: c2 +0.9 %, c3 +1.9 % over two-row slices (same box,
+    // profiles/r5/README.md).  (MP2VG_MATES=0 in dev builds: two-row slices.)
+    static const bool mates = !dev_env("MP2VG_MATES") || atoi(dev_env("MP2VG_MATES")) != 0;
     static const int rows_i = dev_env("MP2VG_SLICE_ROWS_I") ? std::max(1, atoi(dev_env("MP2VG_SLICE_ROWS_I"))) : 1;
     for (int set = 0; set < nsets; set++)
     for (int q = 0; q <= maxlevel; q++) {
@@ -678,7 +683,7 @@ static int plan_batch(mp2vg_ctx_t* c, const mp2vg_picture_t* pics, int32_t npics
                 if (!share) break;
                 j++;
             }
-            const int slice_rows = (mbw % 4 != 0) ? 1 : (types == 1 ? rows_i : rows_pb);
+            const int slice_rows = (mbw % 4 != 0) ? 1 : (types == 1 ? rows_i : (mates ? 1 : rows_pb));
             for (int r = 0; r < mbh; r += slice_rows)
                 for (size_t k = i; k < j; k++)
                     slices.push_back({(uint32_t)lp[k], pics[lp[k]].mb_first + (uint32_t)(r * mbw),
@@ -703,6 +708,7 @@ static int plan_batch(mp2vg_ctx_t* c, const mp2vg_picture_t* pics, int32_t npics
         }
         l.level = q;
         l.set = set;
+        l.mates = mates && types != 1 && l.mcm != 0 && l.mcm != 4 && mbw % 4 == 0;
         if (tplan)
             for (int p : lp)
                 if (need[p] && (pics[p].picture_coding_type == 3 || l.mcm == 4))
@@ -927,6 +933,7 @@ extern "C" int mp2vg_batch_decode(mp2vg_ctx_t* c) {
             }
             a.slice_base = launches[i].begin;
             a.nslices = launches[i].end - launches[i].begin;
+            a.mates = launches[i].mates ? 1u : 0u;
             if (c->launch_timing) HIPCHK(hipEventRecord(H.l[2 * i], st));
             if (a.nslices) HIPCHK(launch_recon(c->g.cf, launches[i].mcm, a, st));
             {  // the launch's pictures that store their tiles by conversion (TilePlan)
