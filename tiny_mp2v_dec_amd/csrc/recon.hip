@@ -787,15 +787,17 @@ struct Lds {
     short res[NWV][C8 ? G * ResLayout<CF>::SIZE / 2 : G * ResLayout<CF>::SIZE];
     uint8_t map[NWV][MAXS];                      // slot -> k*16 + b
     uint32_t dq[NWV][64];                        // (k*16 + b) -> dequant parameters (DqEntry)
-    // quantiser matrices and scan (C8: the I kernels' one picture per workgroup; P/B layouts two
-    // sets, one per half of the workgroup when it runs two slices, recon_kernel `mates`)
-    uint8_t W[C8 ? 4 : 8][64];
+    // quantiser matrices and scan (C8: the I kernels' one picture per workgroup; P/B layouts NH
+    // sets, one per slice when the workgroup runs several, recon_kernel `mates`; 4:4:4 two, so
+    // three workgroups still share a CU)
+    static constexpr int NH = C8 ? 1 : (CF == 3 ? 2 : 4);
+    uint8_t W[4 * NH][64];
     // I kernels (WB): the intra matrix row of each block b (W[0] for b < 6, W[2] above), so a
     // coefficient word's (b, i) bits 16-25 index it directly; scan positions stored doubled (byte
     // offsets of an int16 in the block).  The table sits after `scan`: c5 is sensitive to where
     // the small tables sit (scan 64 B further on: -5 %; the table in front of scan: -1 %)
     static constexpr bool WB = C8;
-    uint8_t scan[C8 ? 64 : 128];
+    uint8_t scan[64 * NH];
     uint8_t Wb[WB && CF != 1 ? Fmt<CF>::NB : 0][64];  // zero-length (clang extension) when unused: no layout change
     // short index of coefficient / pass-1 output idx (0..63) of a slot, relative to the wave's blk
     __device__ static int bofs(int slot, int idx) { return slot * BLK + (C8 ? (idx ^ ((slot & 7) << 3)) : idx); }
@@ -881,7 +883,7 @@ struct SliceCtx {
     __amdgpu_buffer_rsrc_t coef_rsrc;  // the batch's words; offsets >= kNoTap read nothing
     uint32_t mb_begin, mb_end;
     // the wave's place among the waves of its slice and their group stride (STEP MBs): 4 waves
-    // per slice, or 2 when the workgroup runs two slices (recon_kernel `mates`, half 0 / 1)
+    // per slice, or 4 / mates when the workgroup runs `mates` slices (recon_kernel; half = which)
     uint32_t wpos, step;
     int half;
 };
@@ -1378,18 +1380,20 @@ __global__ __launch_bounds__((64 * kernel_waves<MCM, ABL>())) __attribute__((amd
     // references -- waves 0-1 on the first, 2-3 on the second.  XCD-aware bijection: XCD x = b % 8
     // owns the contiguous unit range [x*q + min(x, r), ...)
     constexpr bool MATES_OK = !LT::COMPACT && LT::NWAVES == 4;
-    const bool two = MATES_OK && mates != 0;
-    const uint32_t nunits = two ? (nslices + 1) / 2 : nslices;
+    const uint32_t spw = MATES_OK && (mates == 2 || mates == 4) && mates <= (uint32_t)LT::NH ? mates : 1u;  // slices per workgroup
+    const bool two = spw > 1;
+    const uint32_t wps = 4u / spw;  // waves per slice
+    const uint32_t nunits = (nslices + spw - 1) / spw;
     const uint32_t b = blockIdx.x, q8 = nunits / 8, r8 = nunits % 8, xcd = b % 8;
     const uint32_t unit = xcd * q8 + min(xcd, r8) + b / 8;
-    const int half = two ? (wave >> 1) : 0;
-    const uint32_t si = two ? 2 * unit + (uint32_t)half : unit;
-    const bool have = si < nslices;  // (the last unit of an odd count has one slice)
-    const SliceDesc sd = slices[slice_base + (have ? si : si - 1)];
+    const int half = two ? (int)((uint32_t)wave / wps) : 0;
+    const uint32_t si = spw * unit + (uint32_t)half;
+    const bool have = si < nslices;  // (the last unit may hold fewer slices)
+    const SliceDesc sd = slices[slice_base + min(si, nslices - 1)];  // in range for every wave
     const mp2vg_picture_t* pic = pics + sd.pic;
     const int alt = pic->alternate_scan & 1;
 
-    if ((two ? (tid & 127) : tid) < 64) {
+    if ((uint32_t)wave % wps == 0 && (two || tid < 64)) {
         ((uint32_t*)L.W)[64 * half + lane] = ((const uint32_t*)pic->W)[lane];
         // blocks sit in LDS pair-interleaved: coefficient (v, u) at (v >> 1) * 16 + u * 2 + (v & 1),
         // so a dword is the (row v, row v + 1) pair of column u that IDCT pass 1 transforms
@@ -1434,8 +1438,8 @@ __global__ __launch_bounds__((64 * kernel_waves<MCM, ABL>())) __attribute__((amd
     c.mb_begin = sd.mb_begin;
     c.mb_end = sd.mb_begin + sd.mb_count;
     c.half = half;
-    c.wpos = two ? (uint32_t)(wave & 1) : (uint32_t)wave;
-    c.step = (two ? 2u : (uint32_t)LT::NWAVES) * G;
+    c.wpos = two ? (uint32_t)wave % wps : (uint32_t)wave;
+    c.step = (two ? wps : (uint32_t)LT::NWAVES) * G;
     if constexpr (MCM == 4) {
         run_slice<CF, 0, ABL, LT, false>(c, geo, L, lane, wave);
     } else if constexpr (MCM < 3) {
@@ -1491,10 +1495,10 @@ __global__ void digest_kernel(const uint64_t* __restrict__ ftab, const int32_t* 
 
 template <int CF, int MCM, int ABL>
 static void launch_one(const KArgs& a, const Geo& g, hipStream_t stream) {
-    const bool two = a.mates && MCM != 0 && MCM != 4 && kernel_waves<MCM, ABL>() == 4;
-    hipLaunchKernelGGL((recon_kernel<CF, MCM, ABL>), dim3(two ? (a.nslices + 1) / 2 : a.nslices),
+    const uint32_t spw = (a.mates == 2 || (a.mates == 4 && CF != 3)) && MCM != 0 && MCM != 4 && kernel_waves<MCM, ABL>() == 4 ? a.mates : 1u;
+    hipLaunchKernelGGL((recon_kernel<CF, MCM, ABL>), dim3((a.nslices + spw - 1) / spw),
                        dim3(64 * kernel_waves<MCM, ABL>()), 0, stream, a.pics, (const uint32_t*)a.mbs, a.coefs,
-                       a.slices, g, a.slice_base, a.nslices, two ? 1u : 0u);
+                       a.slices, g, a.slice_base, a.nslices, spw);
 }
 
 template <int CF, int ABL>

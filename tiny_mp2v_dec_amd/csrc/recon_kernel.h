@@ -36,7 +36,7 @@ struct SliceDesc {
 struct Launch {
     uint32_t begin, end;
     int mcm;
-    bool mates = false;  // two consecutive one-row slices (cluster mates) per workgroup
+    int mates = 0;  // consecutive one-row slices (cluster mates) per workgroup: 0 / 2 / 4
     int level;  // dependency level: launches of one level may run concurrently
     int set;    // independent picture set (its own stream)
 };
@@ -65,7 +65,7 @@ struct KArgs {
     int32_t ph[3];
     uint32_t slice_base;
     uint32_t nslices;
-    uint32_t mates = 0;  // P/B launches: two consecutive slices per workgroup (Launch.mates)
+    uint32_t mates = 0;  // P/B launches: consecutive slices per workgroup, 2 or 4 (Launch.mates)
 };
 
 // decoded slots -> host (or HBM) frames of one drop-in chunk, by a copy kernel (recon.hip);

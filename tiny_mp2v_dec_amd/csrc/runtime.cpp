@@ -637,7 +637,7 @@ static int plan_batch(mp2vg_ctx_t* c, const mp2vg_picture_t* pics, int32_t npics
     // one picture (15 groups per wave), half the MB rows in flight per XCD, and both pictures'
     // taps of one anchor region on one CU: c2 +0.9 %, c3 +1.9 % over two-row slices (same box,
     // profiles/r5/README.md).  (MP2VG_MATES=0 in dev builds: two-row slices.)
-    static const bool mates = !dev_env("MP2VG_MATES") || atoi(dev_env("MP2VG_MATES")) != 0;
+    static const int mates = !dev_env("MP2VG_MATES") ? 2 : atoi(dev_env("MP2VG_MATES")) == 4 ? 4 : (atoi(dev_env("MP2VG_MATES")) ? 2 : 0);
     static const int rows_i = dev_env("MP2VG_SLICE_ROWS_I") ? std::max(1, atoi(dev_env("MP2VG_SLICE_ROWS_I"))) : 1;
     for (int set = 0; set < nsets; set++)
     for (int q = 0; q <= maxlevel; q++) {
@@ -708,7 +708,8 @@ static int plan_batch(mp2vg_ctx_t* c, const mp2vg_picture_t* pics, int32_t npics
         }
         l.level = q;
         l.set = set;
-        l.mates = mates && types != 1 && l.mcm != 0 && l.mcm != 4 && mbw % 4 == 0;
+        // (4:4:4 kernels hold two slices' tables at most: Lds::NH)
+        l.mates = (mates && types != 1 && l.mcm != 0 && l.mcm != 4 && mbw % 4 == 0) ? (c->g.cf == 3 ? std::min(mates, 2) : mates) : 0;
         if (tplan)
             for (int p : lp)
                 if (need[p] && (pics[p].picture_coding_type == 3 || l.mcm == 4))
@@ -933,7 +934,7 @@ extern "C" int mp2vg_batch_decode(mp2vg_ctx_t* c) {
             }
             a.slice_base = launches[i].begin;
             a.nslices = launches[i].end - launches[i].begin;
-            a.mates = launches[i].mates ? 1u : 0u;
+            a.mates = (uint32_t)launches[i].mates;
             if (c->launch_timing) HIPCHK(hipEventRecord(H.l[2 * i], st));
             if (a.nslices) HIPCHK(launch_recon(c->g.cf, launches[i].mcm, a, st));
             {  // the launch's pictures that store their tiles by conversion (TilePlan)
