@@ -638,6 +638,11 @@ static int plan_batch(mp2vg_ctx_t* c, const mp2vg_picture_t* pics, int32_t npics
     // taps of one anchor region on one CU: c2 +0.9 %, c3 +1.9 % over two-row slices (same box,
     // profiles/r5/README.md).  (MP2VG_MATES=0 in dev builds: two-row slices.)
     static const int mates = !dev_env("MP2VG_MATES") ? 2 : atoi(dev_env("MP2VG_MATES")) == 4 ? 4 : (atoi(dev_env("MP2VG_MATES")) ? 2 : 0);
+    // An odd cluster's two-reference pictures are mates row by row and its one-reference picture
+    // is its own mate (two consecutive rows): one-stream c2 span -0.8 to -1.5 %, the P / one-
+    // direction B level launch -1.5 to -2.3 % (same box, profiles/r5/README.md).  (MP2VG_PAIR_ORDER=0
+    // in dev builds: plain row-by-row interleave.)
+    static const bool pair_order = !dev_env("MP2VG_PAIR_ORDER") || atoi(dev_env("MP2VG_PAIR_ORDER")) != 0;
     static const int rows_i = dev_env("MP2VG_SLICE_ROWS_I") ? std::max(1, atoi(dev_env("MP2VG_SLICE_ROWS_I"))) : 1;
     for (int set = 0; set < nsets; set++)
     for (int q = 0; q <= maxlevel; q++) {
@@ -684,10 +689,28 @@ static int plan_batch(mp2vg_ctx_t* c, const mp2vg_picture_t* pics, int32_t npics
                 j++;
             }
             const int slice_rows = (mbw % 4 != 0) ? 1 : (types == 1 ? rows_i : (mates ? 1 : rows_pb));
-            for (int r = 0; r < mbh; r += slice_rows)
+            auto push = [&](size_t k, int r) {
+                slices.push_back({(uint32_t)lp[k], pics[lp[k]].mb_first + (uint32_t)(r * mbw),
+                                  (uint32_t)(std::min(slice_rows, mbh - r) * mbw), sflags(lp[k])});
+            };
+            const bool paired = pair_order && mates == 2 && types != 1 && mbw % 4 == 0;
+            if (paired && (j - i) % 2 == 1 && j - i > 1) {
+                // an odd cluster (the P picture and the two B pictures before it): the B pictures,
+                // which share both references, are mates row by row, and the odd one (the
+                // one-reference picture) is its own mate, two consecutive rows
+                size_t o = j - 1;
                 for (size_t k = i; k < j; k++)
-                    slices.push_back({(uint32_t)lp[k], pics[lp[k]].mb_first + (uint32_t)(r * mbw),
-                                      (uint32_t)(std::min(slice_rows, mbh - r) * mbw), sflags(lp[k])});
+                    if (pics[lp[k]].picture_coding_type == 2 || one_dir(lp[k])) o = k;
+                for (int r = 0; r < mbh; r += 2) {
+                    for (int rr = r; rr < std::min(r + 2, mbh); rr++)
+                        for (size_t k = i; k < j; k++)
+                            if (k != o) push(k, rr);
+                    for (int rr = r; rr < std::min(r + 2, mbh); rr++) push(o, rr);
+                }
+            } else {
+                for (int r = 0; r < mbh; r += slice_rows)
+                    for (size_t k = i; k < j; k++) push(k, r);
+            }
             i = j;
         }
         l.end = (uint32_t)slices.size();
