@@ -111,6 +111,10 @@ struct Bank {
     size_t cap_slices = 0;
     int32_t* d_post = nullptr;  // TilePlan.post slots, in launch order (post_of[i]: launch i's range)
     size_t cap_post = 0;
+    // pinned staging of the bank's small arrays (pictures, slices, post lists) for the
+    // asynchronous uploads of the drop-in decoder: copied without a host wait
+    uint8_t* h_small = nullptr;
+    size_t cap_small = 0;
     std::vector<std::pair<int32_t, int32_t>> post_of;
     std::vector<Launch> launches;  // slice ranges per (dependency level, picture type)
     std::vector<std::vector<int32_t>> foot;  // per picture set: the slots it writes or reads
@@ -273,6 +277,7 @@ extern "C" int mp2vg_destroy(mp2vg_ctx_t* c) {
         hipFree(b.d_coefs);
         hipFree(b.d_slices);
         hipFree(b.d_post);
+        if (b.h_small) hipHostFree(b.h_small);
         if (b.uploaded) hipEventDestroy(b.uploaded);
         if (b.consumed) hipEventDestroy(b.consumed);
     }
@@ -765,11 +770,48 @@ static int batch_upload(mp2vg_ctx_t* c, const mp2vg_picture_t* pics, int32_t npi
     // the kernel loads 128 words from the first coefficient of each MB group unconditionally
     if ((rc = grow(b.d_coefs, b.cap_coefs, (size_t)ncoefs + kCoefPad)) != MP2VG_OK) return rc;
     if ((rc = grow(b.d_slices, b.cap_slices, slices.size())) != MP2VG_OK) return rc;
-    // picture records (small, may sit in pageable memory either way) and this function's own
-    // slice descriptors go through staging first: the staged copies end synchronised
-    if ((rc = upload(c, b.d_pics, pics, sizeof(mp2vg_picture_t) * npics, false)) != MP2VG_OK) return rc;
-    if ((rc = upload(c, b.d_slices, slices.data(), sizeof(SliceDesc) * slices.size(), false)) != MP2VG_OK)
-        return rc;
+    // the post-launch tile conversions' slot lists, grouped by launch
+    std::vector<int32_t> ps;
+    std::vector<std::pair<int32_t, int32_t>> post_of(lb.size(), {0, 0});
+    for (size_t i = 0; i < lb.size(); i++) {
+        post_of[i].first = (int32_t)ps.size();
+        for (const auto& pc : tplan.post)
+            if (pc.first == (int32_t)i) ps.push_back(pc.second);
+        post_of[i].second = (int32_t)ps.size();
+    }
+    if (!ps.empty() && (rc = grow(b.d_post, b.cap_post, ps.size())) != MP2VG_OK) return rc;
+    const size_t pic_bytes = sizeof(mp2vg_picture_t) * npics, sl_bytes = sizeof(SliceDesc) * slices.size(),
+                 ps_bytes = sizeof(int32_t) * ps.size();
+    if (async) {
+        // the drop-in's asynchronous upload: the small arrays go through the bank's own pinned
+        // staging block, with no host wait (a synchronised staged copy would wait for the previous
+        // chunk's record copies: the chunk loop then ran at the H2D rate, 0.6 ms per 16 frames).
+        // The block's previous copies finished before the bank's previous decode, waited for above.
+        HIPCHK(hipEventSynchronize(b.uploaded));
+        const size_t o1 = (pic_bytes + 255) & ~(size_t)255, o2 = o1 + ((sl_bytes + 255) & ~(size_t)255);
+        const size_t need = o2 + ps_bytes;
+        if (need > b.cap_small) {
+            if (b.h_small) HIPCHK(hipHostFree(b.h_small));
+            b.h_small = nullptr;
+            b.cap_small = 0;
+            const size_t cap = std::max(need, (size_t)1 << 20);
+            HIPCHK(hipHostMalloc((void**)&b.h_small, cap, hipHostMallocDefault));
+            b.cap_small = cap;
+        }
+        memcpy(b.h_small, pics, pic_bytes);
+        memcpy(b.h_small + o1, slices.data(), sl_bytes);
+        if (ps_bytes) memcpy(b.h_small + o2, ps.data(), ps_bytes);
+        HIPCHK(hipMemcpyAsync(b.d_pics, b.h_small, pic_bytes, hipMemcpyHostToDevice, c->ustream));
+        HIPCHK(hipMemcpyAsync(b.d_slices, b.h_small + o1, sl_bytes, hipMemcpyHostToDevice, c->ustream));
+        if (ps_bytes) HIPCHK(hipMemcpyAsync(b.d_post, b.h_small + o2, ps_bytes, hipMemcpyHostToDevice, c->ustream));
+    } else {
+        // picture records (small, may sit in pageable memory either way), this function's own
+        // slice descriptors and post lists go through staging first: the staged copies end
+        // synchronised
+        if ((rc = upload(c, b.d_pics, pics, pic_bytes, false)) != MP2VG_OK) return rc;
+        if ((rc = upload(c, b.d_slices, slices.data(), sl_bytes, false)) != MP2VG_OK) return rc;
+        if (ps_bytes && (rc = upload(c, b.d_post, ps.data(), ps_bytes, false)) != MP2VG_OK) return rc;
+    }
     if ((rc = upload(c, b.d_mbs, mbs, sizeof(mp2vg_mb_t) * nmbs, pinned)) != MP2VG_OK) return rc;
     if (ncoefs && (rc = upload(c, b.d_coefs, coefs, sizeof(uint32_t) * ncoefs, pinned)) != MP2VG_OK) return rc;
     HIPCHK(hipEventRecord(b.uploaded, c->ustream));
@@ -779,20 +821,7 @@ static int batch_upload(mp2vg_ctx_t* c, const mp2vg_picture_t* pics, int32_t npi
     trace_phase("upload: copy", tp);
     b.launches = std::move(lb);
     b.foot = std::move(foot);
-    {  // the post-launch tile conversions' slot lists, grouped by launch
-        std::vector<int32_t> ps;
-        b.post_of.assign(b.launches.size(), {0, 0});
-        for (size_t i = 0; i < b.launches.size(); i++) {
-            b.post_of[i].first = (int32_t)ps.size();
-            for (const auto& pc : tplan.post)
-                if (pc.first == (int32_t)i) ps.push_back(pc.second);
-            b.post_of[i].second = (int32_t)ps.size();
-        }
-        if (!ps.empty()) {
-            if ((rc = grow(b.d_post, b.cap_post, ps.size())) != MP2VG_OK) return rc;
-            if ((rc = upload(c, b.d_post, ps.data(), sizeof(int32_t) * ps.size(), false)) != MP2VG_OK) return rc;
-        }
-    }
+    b.post_of = std::move(post_of);
     b.tiles = std::move(tplan);
     b.npics = npics;
     c->cur = k;

@@ -1,0 +1,30 @@
+"""Drop-in end to end, repeated, with the native phase trace (dev tool, run on the GPU box): the c2
+bench stream (64 GOPs) decoded 6 times by one mp2v_decoder_c (host frames, 16 threads); prints
+frames/s per run, and MP2VG_TRACE's per-phase lines go to stderr, for telling a slow run's phase.
+
+    MP2VG_TRACE=1 python tools/dropin_trace.py [gops] 2> trace.txt
+"""
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
+from tiny_mp2v_dec_amd import records as R  # noqa: E402
+from tiny_mp2v_dec_amd.decoder import decoder_config_t, mp2v_decoder_c  # noqa: E402
+
+gops = int(sys.argv[1]) if len(sys.argv) > 1 else 64
+w, h, cf, extra, _ = bench.CONFIGS["c2"]
+es = R.generate_es(width=w, height=h, chroma_format=cf, n_gops=gops, seed=1729, **extra)
+n = [0]
+dec = mp2v_decoder_c(decoder_config_t(w, h, cf, pictures_pool_size=24, num_threads=16),
+                     lambda f: n.__setitem__(0, n[0] + 1))
+for run in range(6):
+    n[0] = 0
+    print(f"=== run {run}", file=sys.stderr, flush=True)
+    t0 = time.perf_counter()
+    dec.decode(es)
+    dt = time.perf_counter() - t0
+    print(json.dumps({"run": run, "frames": n[0], "frames_per_s": round(n[0] / dt, 1)}), flush=True)
+dec.close()
