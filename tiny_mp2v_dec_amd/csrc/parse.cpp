@@ -136,6 +136,12 @@ struct Ctx {
         return;                  \
     } while (0)
 
+// 6-bit reversal: coded_block_pattern bit (5 - i) names block i
+static const uint8_t kRev6[64] = {
+    0,  32, 16, 48, 8,  40, 24, 56, 4,  36, 20, 52, 12, 44, 28, 60, 2,  34, 18, 50, 10, 42,
+    26, 58, 6,  38, 22, 54, 14, 46, 30, 62, 1,  33, 17, 49, 9,  41, 25, 57, 5,  37, 21, 53,
+    13, 45, 29, 61, 3,  35, 19, 51, 11, 43, 27, 59, 7,  39, 23, 55, 15, 47, 31, 63};
+
 // One slice -> its MB row of records (mb_decoder.cpp:521-641 for every MB of the slice).
 void parse_slice(const Ctx& C, const PicWork& P, const SliceJob& job, mp2vg_mb_t* row_base_all,
                  std::atomic<uint8_t>* row_done, SliceOut& out) {
@@ -352,14 +358,10 @@ void parse_slice(const Ctx& C, const PicWork& P, const SliceJob& job, mp2vg_mb_t
             uint32_t c1 = 0, c2 = 0;
             if (cf == 2) c1 = br.read(2);
             if (cf == 3) c2 = br.read(6);
-            for (int i = 0; i < 6; i++)
-                if (v & (1u << (5 - i))) cbp |= 1u << i;
-            if (cf == 2)
-                for (int i = 6; i < 8; i++)
-                    if (c1 & (1u << (7 - i))) cbp |= 1u << i;
-            if (cf == 3)
-                for (int i = 6; i < 12; i++)
-                    if (c2 & (1u << (11 - i))) cbp |= 1u << i;
+            // block i <- bit (5 - i) of the code (6.3.17.4), a 6-bit reversal (no branch per bit)
+            cbp |= kRev6[v & 63];
+            if (cf == 2) cbp |= (uint32_t)(((c1 & 1) << 1) | ((c1 >> 1) & 1)) << 6;
+            if (cf == 3) cbp |= (uint32_t)kRev6[c2 & 63] << 6;
         }
         cbp &= (1u << nblocks) - 1;
         if (dct_type && (intra || pattern)) m.flags |= MP2VG_MB_DCT_FIELD;
@@ -382,8 +384,9 @@ void parse_slice(const Ctx& C, const PicWork& P, const SliceJob& job, mp2vg_mb_t
         BitReader r = br;
         const uint32_t* const lut1 = cf_lut.l1.data();
         const uint32_t* const lut2 = cf_lut.l2.data();
-        for (int b = 0; b < nblocks; b++) {
-            if (!(cbp & (1u << b))) continue;
+        // the coded blocks only, lowest first (no data-dependent branch per block position)
+        for (uint32_t bits = cbp; bits; bits &= bits - 1) {
+            const int b = __builtin_ctz(bits);
             int i = 0;
             const uint32_t btag = ((uint32_t)b << 22) | mbx_tag;  // MP2VG_COEF_PACK's block field
             if (intra) {
@@ -403,14 +406,14 @@ void parse_slice(const Ctx& C, const PicWork& P, const SliceJob& job, mp2vg_mb_t
                 *w++ = MP2VG_COEF_PACK(dcv, 0, b, MP2VG_COEF_DC | MP2VG_COEF_MBX(x));
                 i = 1;
             } else {
-                // non-intra first coefficient '1s' (mb_decoder.cpp:79-88)
-                uint32_t c = r.peek(2);
-                if (c & 2) {
-                    int lvl = (c & 1) ? -1 : 1;
-                    *w++ = MP2VG_COEF_PACK(lvl, 0, b, MP2VG_COEF_FIRST1S | MP2VG_COEF_MBX(x));
-                    r.skip(2);
-                    i = 1;
-                }
+                // non-intra first coefficient '1s' (mb_decoder.cpp:79-88), without a branch: the
+                // word is stored and kept (w advanced, the two bits consumed) when the bits are '1s'
+                const uint32_t c = r.peek(2);
+                const uint32_t f = c >> 1;
+                *w = MP2VG_COEF_PACK(1 - 2 * (int)(c & 1), 0, b, MP2VG_COEF_FIRST1S | MP2VG_COEF_MBX(x));
+                w += f;
+                r.skip_nr(2 * (int)f);
+                i = (int)f;
             }
             // parse_block's VLC loop (mb_decoder.cpp:89-149): one refill per two codes (a refill
             // leaves >= 56 bits; a code takes at most 24, an escape)
