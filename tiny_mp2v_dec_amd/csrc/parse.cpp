@@ -268,15 +268,19 @@ void parse_slice(const Ctx& C, const PicWork& P, const SliceJob& job, mp2vg_mb_t
         int fsel[2][2] = {};
         // (always inline: an out-of-line lambda takes br's address and keeps the slice's bit
         // reader in memory, a store-forwarding round trip on every read)
+        // one lookup for motion_code and its sign, the residual read with a width of 0 when
+        // there is none (f_code 1 or code 0): no branch on the code's value
         auto parse_mv = [&](int r, int s) __attribute__((always_inline)) -> bool {
             for (int t = 0; t < 2; t++) {
-                int ci = T.motion.decode(br);
-                if (ci < 0) return false;
-                int mc = kMotionCodes[ci].a;
-                if (mc && br.read(1)) mc = -mc;
-                int fc = h.f_code[s][t];
-                int residual = 0;
-                if (fc != 1 && mc != 0) residual = (int)br.read(fc - 1);
+                br.refill();  // >= 56 bits: code and sign <= 11, residual <= 8
+                const uint32_t e = T.motion_signed[br.peek_nr(11)];
+                if (!e) return false;
+                br.skip_nr((int)(e >> 16));
+                const int mc = (int)(e & 0xffffu) - 32;
+                const int fc = h.f_code[s][t];
+                const int n = mc != 0 ? fc - 1 : 0;
+                const int residual = (int)(((br.cache >> 1) >> (63 - n)) & ((1u << n) - 1u));
+                br.skip_nr(n);
                 MVs[r][s][t] = mv_reconstruct(fc, mc, residual, PMVs[r][s][t], field_mv && t == 1);
             }
             return true;

@@ -207,6 +207,9 @@ struct CoefLut {
 
 struct Tables {
     VlcLut mba, mbtype[4], cbp, motion, dc_luma, dc_chroma;
+    // motion_code with its sign folded in (B.10 + the sign bit of a non-zero code), 11-bit index:
+    // entry = (bits consumed << 16) | (motion_code + 32), 0 = invalid
+    std::vector<uint32_t> motion_signed;
     CoefLut coefs[2];
     static const Tables& get();
 };
@@ -229,13 +232,12 @@ inline int16_t mv_reconstruct(int f_code, int motion_code, int residual, int16_t
     int r_size = f_code - 1;
     int f = 1 << r_size;
     int high = 16 * f - 1, low = -16 * f, range = 32 * f;
-    int delta;
-    if (f != 1 && motion_code != 0) {
-        delta = ((motion_code < 0 ? -motion_code : motion_code) - 1) * f + residual + 1;
-        if (motion_code < 0) delta = -delta;
-    } else {
-        delta = motion_code;
-    }
+    // (|code| - 1) * f + residual + 1 with the code's sign, 0 for code 0; f = 1 carries no
+    // residual, so the same form gives the code itself (no branch on the code's value)
+    const int a = motion_code < 0 ? -motion_code : motion_code;
+    const int d = (a - 1) * f + residual + 1;
+    int delta = motion_code < 0 ? -d : d;
+    delta = motion_code != 0 ? delta : 0;
     int prediction = field_vert ? (PMV >> 1) : PMV;
     int mv = prediction + delta;
     if (mv < low) mv += range;

@@ -78,6 +78,19 @@ static Tables* build_tables() {
     add_list(t->cbp, kCbpCodes);
     t->motion.init(10);
     add_list(t->motion, kMotionCodes);
+    t->motion_signed.assign(1u << 11, 0);
+    for (const vlc_code& m : kMotionCodes) {
+        const int len = (int)strlen(m.bits);
+        uint32_t code = 0;
+        for (int i = 0; i < len; i++) code = (code << 1) | (m.bits[i] == '1');
+        for (int sign = 0; sign < (m.a ? 2 : 1); sign++) {
+            const int n = m.a ? len + 1 : len;
+            const uint32_t c = m.a ? (code << 1) | (uint32_t)sign : code;
+            const int v = sign ? -m.a : m.a;
+            for (uint32_t x = c << (11 - n); x < (c + 1) << (11 - n); x++)
+                t->motion_signed[x] = ((uint32_t)n << 16) | (uint32_t)(v + 32);
+        }
+    }
     t->dc_luma.init(9);
     add_list(t->dc_luma, kDcSizeLuma);
     t->dc_chroma.init(10);
