@@ -396,15 +396,14 @@ void parse_slice(const Ctx& C, const PicWork& P, const SliceJob& job, mp2vg_mb_t
             if (intra) {
                 // parse_dct_dc_coeff (mb_decoder.cpp:46-72)
                 int pidx = b < 4 ? 0 : ((b & 1) ? 2 : 1);
-                int si = (b < 4 ? T.dc_luma : T.dc_chroma).decode(r);
+                int si = (b < 4 ? T.dc_luma : T.dc_chroma).decode(r);  // (refilled: >= 46 bits left)
                 if (si < 0) FAIL(MP2VG_E_BITSTREAM, "bad dct_dc_size");
-                int size = (b < 4 ? kDcSizeLuma : kDcSizeChroma)[si].a;
-                int diff = 0;
-                if (size) {
-                    int d = (int)r.read(size);
-                    int half = 1 << (size - 1);
-                    diff = d >= half ? d : (d + 1) - 2 * half;
-                }
+                const int size = (b < 4 ? kDcSizeLuma : kDcSizeChroma)[si].a;  // <= 11
+                // dct_dc_differential of `size` bits (none for size 0), without a branch on size
+                const int d = (int)(((r.cache >> 1) >> (63 - size)) & ((1u << size) - 1u));
+                r.skip_nr(size);
+                const int half = (1 << size) >> 1;
+                const int diff = d >= half ? d : (d + 1) - 2 * half;
                 dc_pred[pidx] = (uint16_t)(dc_pred[pidx] + diff);
                 int16_t dcv = (int16_t)(dc_pred[pidx] << (3 - h.intra_dc_precision));
                 *w++ = MP2VG_COEF_PACK(dcv, 0, b, MP2VG_COEF_DC | MP2VG_COEF_MBX(x));

@@ -162,7 +162,8 @@ struct VlcLut {
 // 5-bit lookup.  The escape (6-bit code, 6-bit run, signed 12-bit level) is decoded without a
 // branch: it is frequent in noisy content (9 % of the codes of the bench stream) and a branch on
 // it mispredicts.
-// Entry: bits 0-4 bits consumed (0 = invalid), 5-10 run, 11-22 signed level, 23-24 kind.
+// Entry: bits 0-4 bits consumed (0 = invalid; an escape's 24: code, run and level), 5-10 run,
+// 11-22 signed level, 23-24 kind.
 struct CoefLut {
     enum { NORMAL = 0, EOB = 1, ESC = 2, SUB = 3, L1 = 12, L2 = 5 };
     std::vector<uint32_t> l1, l2;  // l2: (1 << L2)-entry sub-tables
@@ -200,7 +201,7 @@ struct CoefLut {
         const uint32_t rl = (rl_norm & ~esc) | (((x >> 12) | ((x & 0xfffu) << 6)) & esc);
         run = (int)(rl & 63);
         level = (int32_t)(rl << 14) >> 20;  // signed 12 bits
-        br.skip_nr(len + (int)(esc & 18u));
+        br.skip_nr(len);  // (an escape's entry length includes its run and level)
         return kind & ~(int)(esc & 2u);  // ESC -> NORMAL
     }
 };

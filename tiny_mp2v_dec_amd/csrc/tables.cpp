@@ -45,7 +45,9 @@ void CoefLut::add(const char* bits, int run, int level, int kind) {
         }
         if (n <= L1) {
             const uint32_t lo = code << (L1 - n), hi = (code + 1) << (L1 - n);
-            for (uint32_t v = lo; v < hi; v++) l1[v] = pack(n, run, lv, kind);
+            // an escape's entry counts its 18 bits of run and level too (decode_entry skips the
+            // entry's length alone: no add on the code-to-code dependency chain)
+            for (uint32_t v = lo; v < hi; v++) l1[v] = pack(kind == ESC ? n + 18 : n, run, lv, kind);
         } else {
             const uint32_t pre = code >> (n - L1);
             uint32_t& e = l1[pre];
