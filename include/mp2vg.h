@@ -360,8 +360,12 @@ int  mp2vg_decoder_frames_allocated(const mp2vg_decoder_t* dec);
 /* lane hand-offs in the last decode() (several lanes): in_flight = times the stream moved to
  * another lane while the lane just left was still downloading its last chunk (the host did not
  * wait: both lanes' chunks in flight at once); blocks = times the host waited for another lane's
- * downloads because the frame pool could not give the next chunk its frames otherwise */
-int  mp2vg_decoder_handoff_stats(const mp2vg_decoder_t* dec, int32_t* in_flight, int32_t* blocks);
+ * downloads because the frame pool could not give the next chunk its frames otherwise; landed =
+ * lane changes where the lane just left had nothing in flight or its downloads were found landed
+ * by the non-blocking check; changes = lane changes.  Every change is in_flight, landed or one of
+ * the blocks.  Any out pointer may be NULL. */
+int  mp2vg_decoder_handoff_stats(const mp2vg_decoder_t* dec, int32_t* in_flight, int32_t* blocks, int32_t* landed,
+                                 int32_t* changes);
 int  mp2vg_decoder_destroy(mp2vg_decoder_t* dec);
 
 #ifdef __cplusplus

@@ -173,7 +173,7 @@ def lib():
         "mp2vg_decoder_stream_headers": ([VP, P(StreamHeaders)], ctypes.c_int),
         "mp2vg_decoder_lane_frames": ([VP, P(I32), I32], ctypes.c_int),
         "mp2vg_decoder_frames_allocated": ([VP], ctypes.c_int),
-        "mp2vg_decoder_handoff_stats": ([VP, P(I32), P(I32)], ctypes.c_int),
+        "mp2vg_decoder_handoff_stats": ([VP, P(I32), P(I32), P(I32), P(I32)], ctypes.c_int),
         "mp2vg_decoder_destroy": ([VP], ctypes.c_int),
     }
     for name, (args, res) in sig.items():

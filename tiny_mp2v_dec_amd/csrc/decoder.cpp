@@ -218,8 +218,9 @@ struct mp2vg_decoder {
     mp2vg_stream_headers_t hdrs{};     // of the last decode()
     // of the last decode(): lane changes that found the lane just left still downloading (its
     // chunk left in flight, the host moving on), and host blocks on another lane's downloads
-    // (only when the frame pool runs short)
-    int handoffs_in_flight = 0, handoff_blocks = 0;
+    // (only when the frame pool runs short); lane changes whose lane just left had nothing in
+    // flight or was completed by the non-blocking check; lane changes
+    int handoffs_in_flight = 0, handoff_blocks = 0, handoffs_landed = 0, lane_changes = 0;
 };
 
 extern "C" int mp2vg_decoder_destroy(mp2vg_decoder_t* d) {
@@ -322,10 +323,13 @@ extern "C" int mp2vg_decoder_lane_frames(const mp2vg_decoder_t* d, int32_t* fram
     return (int)d->lanes.size();
 }
 
-extern "C" int mp2vg_decoder_handoff_stats(const mp2vg_decoder_t* d, int32_t* in_flight, int32_t* blocks) {
+extern "C" int mp2vg_decoder_handoff_stats(const mp2vg_decoder_t* d, int32_t* in_flight, int32_t* blocks,
+                                           int32_t* landed, int32_t* changes) {
     if (!d) return MP2VG_E_INVALID;
     if (in_flight) *in_flight = d->handoffs_in_flight;
     if (blocks) *blocks = d->handoff_blocks;
+    if (landed) *landed = d->handoffs_landed;
+    if (changes) *changes = d->lane_changes;
     return MP2VG_OK;
 }
 
@@ -635,7 +639,7 @@ extern "C" int mp2vg_decoder_decode(mp2vg_decoder_t* d, const uint8_t* buf, uint
     // advance in decode order and every lane decodes while the next one is being fed
     Lane* prev = nullptr;
     uint64_t seq = 0;
-    d->handoffs_in_flight = d->handoff_blocks = 0;
+    d->handoffs_in_flight = d->handoff_blocks = d->handoffs_landed = d->lane_changes = 0;
     for (int s = 0; s < npics;) {
         Lane& L = lane_of(s);
         int e = s + 1;
@@ -645,9 +649,16 @@ extern "C" int mp2vg_decoder_decode(mp2vg_decoder_t* d, const uint8_t* buf, uint
         // several lanes every lane's chunk can be in flight at once.  Only when the frame pool
         // could not give this chunk its frames without growing does the host wait, for the
         // oldest pending lane first (its frames come first in display order).
+        const bool change = nl > 1 && prev && prev != &L;
+        // a lane change is counted once: the lane just left had nothing in flight or its downloads
+        // had landed (non-blocking check: `landed`), it is left in flight, or the host waited for it
+        bool landed = change && prev->pend.empty();
         if (nl > 1) {
-            for (auto& Xp : d->lanes)
+            for (auto& Xp : d->lanes) {
+                const bool was = change && Xp.get() == prev && !Xp->pend.empty();
                 if (Xp.get() != &L && (rc = try_complete(*Xp)) < 0) return finish(rc);
+                if (was && Xp->pend.empty()) landed = true;
+            }
             FramePool& pool = d->device_frames ? *L.dpool : *d->hpool;
             for (;;) {
                 if (pool.free_count() >= (size_t)(e - s)) break;
@@ -661,7 +672,11 @@ extern "C" int mp2vg_decoder_decode(mp2vg_decoder_t* d, const uint8_t* buf, uint
         }
         if ((rc = run_chunk(L, s, e)) != MP2VG_OK) return finish(rc);
         L.pend_seq = seq++;
-        if (prev && prev != &L && !prev->pend.empty()) d->handoffs_in_flight++;
+        if (change) {
+            d->lane_changes++;
+            if (!prev->pend.empty()) d->handoffs_in_flight++;
+            else if (landed) d->handoffs_landed++;
+        }
         prev = &L;
         s = e;
     }

@@ -543,7 +543,10 @@ __device__ __forceinline__ void row_store8(uint8_t* d, uint32_t a, uint32_t b) {
 //   tiles nt (streaming: the lines stay in L2 but go first)  +4.0-4.8 %  (the I launch -10-13 %)
 //   tiles sc1 (write through, line dropped from L2)           -0.2 %
 //   tiles nt + sc1                                            +1.6 %
-//   rows sc1 (no kernel reads the frame_c rows back)          +1.5 % alone, +0.5 % over tiles nt
+//   rows sc1 (write-through: no later recon launch reads the   +1.5 % alone, +0.5 % over tiles nt
+//            frame_c rows -- the taps read the tiles -- but tile_convert (after a mode-4 I launch,
+//            for B pictures read later, for invalidated slots), digest_kernel and the drop-in's
+//            frame_copy_kernel do, after the launch boundary; the A/B covers the c2 P/B path)
 //   rows nt                                                   -3.5 % over tiles nt
 //   records + coefficient words nt loads                      -0.5 %
 #ifndef MP2VG_ROW_POL
@@ -768,6 +771,22 @@ __device__ __forceinline__ void tile_group(uint32_t mx0, uint32_t mby, int lane,
 }
 
 // ---- one slice ------------------------------------------------------------------------------
+// Slices per workgroup (`mates`, recon_kernel): 2 or 4 cluster-mate slices in the 4-wave P/B
+// kernels, at most as many as the LDS holds matrix sets (Lds::NH: 4, or 2 in 4:4:4); 1 otherwise.
+// The one rule for the host's grid size (launch_one) and the kernel's slice index.
+// dev ablations that keep the I kernels' compact layout: 16 stamps, 32768 none, 65536 tile stores
+// into a 64-KB window of the tile slot (L2-resident: the stores' memory traffic, not their issue)
+constexpr int kAblCompact = 16 | 32768 | 65536;
+template <int MCM, int ABL>
+constexpr bool compact_layout() { return (MCM == 0 || MCM == 4) && (ABL & ~kAblCompact) == 0; }
+constexpr int lds_sets(int cf, bool c8) { return c8 ? 1 : (cf == 3 ? 2 : 4); }
+template <int CF, int MCM, int ABL>
+constexpr uint32_t slices_per_wg(uint32_t mates) {
+    return !compact_layout<MCM, ABL>() && kernel_waves<MCM, ABL>() == 4 && (mates == 2 || mates == 4) &&
+                   mates <= (uint32_t)lds_sets(CF, false)
+               ? mates
+               : 1u;
+}
 constexpr int BLKS = 72;
 // C8 = the compact layout of the I kernels (4:4:4: 38.4 KB instead of 53.8 KB per workgroup, so
 // four workgroups share a CU instead of three; 4:2:2 26.0 KB, 4:2:0 19.9 KB)
@@ -790,7 +809,7 @@ struct Lds {
     // quantiser matrices and scan (C8: the I kernels' one picture per workgroup; P/B layouts NH
     // sets, one per slice when the workgroup runs several, recon_kernel `mates`; 4:4:4 two, so
     // three workgroups still share a CU)
-    static constexpr int NH = C8 ? 1 : (CF == 3 ? 2 : 4);
+    static constexpr int NH = lds_sets(CF, C8);
     uint8_t W[4 * NH][64];
     // I kernels (WB): the intra matrix row of each block b (W[0] for b < 6, W[2] above), so a
     // coefficient word's (b, i) bits 16-25 index it directly; scan positions stored doubled (byte
@@ -1353,10 +1372,6 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, LT&
     }
 }
 
-// dev ablations that keep the I kernels' compact layout: 16 stamps, 32768 none, 65536 tile stores
-// into a 64-KB window of the tile slot (L2-resident: the stores' memory traffic, not their issue)
-constexpr int kAblCompact = 16 | 32768 | 65536;
-
 // Occupancy targets per kernel from its LDS: 4:2:0 / 4:2:2 P/B workgroups fit 4 per CU (128
 // VGPRs), 4:4:4 P/B 3 (168 VGPRs cost nothing); the compact I kernels fit 4 (4:4:4) or 6 (80 VGPRs)
 template <int CF, int MCM, int ABL = 0>
@@ -1370,7 +1385,7 @@ __global__ __launch_bounds__((64 * kernel_waves<MCM, ABL>())) __attribute__((amd
                                                     const Geo geo,
                                                     const uint32_t slice_base, const uint32_t nslices,
                                                     const uint32_t mates) {
-    using LT = Lds<CF, (MCM == 0 || MCM == 4) && (ABL & ~kAblCompact) == 0, kernel_waves<MCM, ABL>()>;
+    using LT = Lds<CF, compact_layout<MCM, ABL>(), kernel_waves<MCM, ABL>()>;
     __shared__ __attribute__((aligned(128))) LT L;  // 128-B aligned: pass1_store
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -1379,8 +1394,8 @@ __global__ __launch_bounds__((64 * kernel_waves<MCM, ABL>())) __attribute__((amd
     // consecutive slices -- cluster mates, the same MB row of two pictures that read the same
     // references -- waves 0-1 on the first, 2-3 on the second.  XCD-aware bijection: XCD x = b % 8
     // owns the contiguous unit range [x*q + min(x, r), ...)
-    constexpr bool MATES_OK = !LT::COMPACT && LT::NWAVES == 4;
-    const uint32_t spw = MATES_OK && (mates == 2 || mates == 4) && mates <= (uint32_t)LT::NH ? mates : 1u;  // slices per workgroup
+    static_assert(slices_per_wg<CF, MCM, ABL>(4) <= (uint32_t)LT::NH, "one matrix set per slice");
+    const uint32_t spw = slices_per_wg<CF, MCM, ABL>(mates);  // the grid's rule (launch_one)
     const bool two = spw > 1;
     const uint32_t wps = 4u / spw;  // waves per slice
     const uint32_t nunits = (nslices + spw - 1) / spw;
@@ -1495,7 +1510,7 @@ __global__ void digest_kernel(const uint64_t* __restrict__ ftab, const int32_t* 
 
 template <int CF, int MCM, int ABL>
 static void launch_one(const KArgs& a, const Geo& g, hipStream_t stream) {
-    const uint32_t spw = (a.mates == 2 || (a.mates == 4 && CF != 3)) && MCM != 0 && MCM != 4 && kernel_waves<MCM, ABL>() == 4 ? a.mates : 1u;
+    const uint32_t spw = slices_per_wg<CF, MCM, ABL>(a.mates);  // the kernel applies the same rule
     hipLaunchKernelGGL((recon_kernel<CF, MCM, ABL>), dim3((a.nslices + spw - 1) / spw),
                        dim3(64 * kernel_waves<MCM, ABL>()), 0, stream, a.pics, (const uint32_t*)a.mbs, a.coefs,
                        a.slices, g, a.slice_base, a.nslices, spw);

@@ -165,10 +165,11 @@ class mp2v_decoder_c:  # noqa: N801  (reference name)
 
     def handoff_stats(self):
         """(lane changes that left the previous lane's chunk in flight, host waits on another
-        lane's downloads) in the last decode() (mp2vg_decoder_handoff_stats)."""
-        a, b = ctypes.c_int32(), ctypes.c_int32()
-        lib().mp2vg_decoder_handoff_stats(self._h, ctypes.byref(a), ctypes.byref(b))
-        return a.value, b.value
+        lane's downloads, lane changes whose lane just left had landed without a wait, lane
+        changes) in the last decode() (mp2vg_decoder_handoff_stats)."""
+        v = [ctypes.c_int32() for _ in range(4)]
+        lib().mp2vg_decoder_handoff_stats(self._h, *[ctypes.byref(x) for x in v])
+        return tuple(x.value for x in v)
 
     def frames_allocated(self):
         """Frame buffers held by the decoder's frame pools (bounded: the renderer back-pressures

@@ -34,6 +34,7 @@ for n in lanes:
     stats = dec.handoff_stats()
     out = {"lanes": n, "frames": frames[0], "frames_per_s": round(frames[0] / dt, 1), "lane_frames": dec.lane_frames(),
            "handoffs_left_in_flight": stats[0], "host_waits_on_other_lane": stats[1],
+           "handoffs_landed": stats[2], "lane_changes": stats[3],
            "frames_allocated": dec.frames_allocated(), "host_threads": threads}
     dec.close()
     print(json.dumps(out), flush=True)
