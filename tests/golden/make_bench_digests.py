@@ -33,6 +33,9 @@ RANKS = 8
 # without this key, or with another value, is never resumed from or merged into.
 DIGEST_FORMAT = bench.DIGEST_FORMAT
 CASES = [("c1", 0)] + [("c2", s) for s in range(RANKS)] + [("c3", 0), ("c4", 0)] + [("c4", s) for s in range(1, RANKS)] + [("c5", 0)]
+# (config, rank, GOPs): one-GOP c4 streams of all 8 ranks, for the 8-rank rehearsal of the c4
+# scaling command (tests/test_bench_multirank.py: bench.py --gpus 8 --config c4 --gops 1)
+CASES += [("c4", s, 1) for s in range(RANKS)]
 
 
 def reference_digests(es, w, h, cf, tmp):
@@ -57,7 +60,7 @@ def reference_digests(es, w, h, cf, tmp):
 def main():
     if not os.path.exists(REF):
         sys.exit("build the reference first: make -C oracle ref")
-    only = set(sys.argv[1:])  # e.g. "c1": (re)compute only these configs, keep the other keys
+    only = set(sys.argv[1:])  # e.g. "c1" or "c4_g1": (re)compute only these cases, keep the other keys
     out = {}
     path = os.path.join(HERE, "bench_digests.npz")
     resume = bool(os.environ.get("MP2VG_DIGESTS_RESUME"))
@@ -72,11 +75,12 @@ def main():
                 out = {k: d[k].copy() for k in d.files}
     out["digest_format"] = np.array([DIGEST_FORMAT], np.int64)
     with tempfile.TemporaryDirectory() as tmp:
-        for config, rank in CASES:
-            if only and config not in only:
+        for case in CASES:
+            config, rank = case[0], case[1]
+            gops = case[2] if len(case) > 2 else bench.DEFAULT_GOPS[config]
+            if only and config not in only and f"{config}_g{gops}" not in only:
                 continue
             w, h, cf, gparams, _ = bench.CONFIGS[config]
-            gops = bench.DEFAULT_GOPS[config]
             seed = 1729 + rank
             if resume and f"{config}_g{gops}_s{seed}" in out:
                 continue  # resuming an interrupted run: keep the finished cases

@@ -53,6 +53,25 @@ def test_bench_plain_gpus_2_spawns_its_ranks_on_one_gpu():
     assert line["parity"]["status"] in ("bit-exact", "unchecked")
 
 
+def test_bench_eight_ranks_c4_gloo_on_one_gpu():
+    """The c4 8-GPU scaling command one step from the driver's: `python bench.py --gpus 8 --config
+    c4 --gops 1 --backend gloo` spawns 8 ranks (all on GPU 0 here; one per GPU on a node), rank r
+    decodes the one-GOP 4K stream of seed 1729 + r, and every rank's 12 frames are checked against
+    the compiled reference's digests (tests/golden/bench_digests.npz, c4_g1_s1729..1736), then
+    rank 0 gathers the first GOP of every rank in display order and checks it frame by frame."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "8", "--config", "c4", "--gops", "1",
+           "--steps", "2", "--warmup", "1", "--backend", "gloo", "--gather-gops", "1"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=REPO, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    assert line["n_gpus"] == 8 and line["config"]["backend"] == "gloo" and line["scaling"] == "weak"
+    assert line["config"]["global_batch_frames"] == 8 * 12
+    assert line["parity"]["status"] == "bit-exact" and line["parity"]["frames_checked"] == 8 * 12
+    g = line["frame_gather"]
+    assert g["verified"] and g["frames"] == 8 * 12
+
+
 def test_bench_one_rank_over_rccl():
     """bench.py's nccl (= RCCL) branch executed for real: one rank under torch.distributed.run
     binds the process group to cuda:0 (device_id: eager communicator init), and the max-over-ranks

@@ -270,10 +270,11 @@ def test_gather_gops_sends_on_the_backend_device():
     assert all(t.device == torch.device("cpu") for _, t, _ in sent)
 
 
-@pytest.mark.parametrize("config,ranks", [("c2", 8), ("c4", 8)])
-def test_reference_digests_for_every_rank_of_the_scaling_run(config, ranks):
+@pytest.mark.parametrize("config,ranks,gops", [("c2", 8, None), ("c4", 8, None), ("c4", 8, 1)])
+def test_reference_digests_for_every_rank_of_the_scaling_run(config, ranks, gops):
     """The driver's 1/2/4/8-GPU bench runs give rank r the stream of seed 1729 + r: the compiled
-    reference's per-frame digests exist for every rank, so parity is checked on all of them."""
+    reference's per-frame digests exist for every rank, so parity is checked on all of them (and
+    for the one-GOP c4 rehearsal of the 8-rank command, tests/test_bench_multirank.py)."""
     import sys
     sys.path[:0] = [REPO]
     import bench
@@ -281,9 +282,10 @@ def test_reference_digests_for_every_rank_of_the_scaling_run(config, ranks):
     with np.load(os.path.join(REPO, "tests", "golden", "bench_digests.npz")) as d:
         # the entries were computed with the formula bench.py's device digests use
         assert int(d["digest_format"][0]) == bench.DIGEST_FORMAT
+    gops = gops or bench.DEFAULT_GOPS[config]
     for r in range(ranks):
-        exp = bench.expected_digests(config, bench.DEFAULT_GOPS[config], 1729 + r)
-        assert exp is not None and len(exp) == 12 * bench.DEFAULT_GOPS[config], (config, r)
+        exp = bench.expected_digests(config, gops, 1729 + r)
+        assert exp is not None and len(exp) == 12 * gops, (config, r)
 
 
 def test_plain_bench_gpus_2_spawns_two_ranks():
@@ -301,6 +303,23 @@ def test_plain_bench_gpus_2_spawns_two_ranks():
     lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
     assert len(lines) == 1  # rank 0 only
     assert lines[0]["n_gpus"] == 2 and lines[0]["ranks"] == [0, 1] and lines[0]["max_rank"] == 1.0
+
+
+def test_plain_bench_gpus_8_c4_spawns_eight_ranks():
+    """The c4 scaling command's launch, `python bench.py --gpus 8 --config c4` with no launcher:
+    eight ranks over gloo form one world, each knows its rank, and max-over-ranks sees all of them."""
+    import json
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "8", "--config", "c4", "--gops", "1",
+                        "--backend", "gloo", "--probe-launch"], capture_output=True, text=True, timeout=300, cwd=repo,
+                       env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1  # rank 0 only
+    assert lines[0]["n_gpus"] == 8 and lines[0]["ranks"] == list(range(8)) and lines[0]["max_rank"] == 7.0
 
 
 def test_bench_refuses_a_world_that_does_not_match_gpus():
