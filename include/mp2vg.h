@@ -202,6 +202,10 @@ int  mp2vg_slot_device_ptr(mp2vg_ctx_t* ctx, int32_t slot, void** dptr);
  * that predicts from the slot rebuilds them from the frame first (tile_convert).  Call it after
  * the writes have completed and before mp2vg_batch_decode of a batch that reads the slot. */
 int  mp2vg_invalidate_slot(mp2vg_ctx_t* ctx, int32_t slot);
+/* diagnostics: device address of the context's kernel sink block (dummy loads and stores of the
+ * decode; from +3072 the per-stage cycle sums of a stamp build, tools/stamps.py).  Never written
+ * by callers. */
+int  mp2vg_sink_device_ptr(mp2vg_ctx_t* ctx, void** dptr);
 /* 64-bit order-independent digest of each listed slot's visible planes, computed on device:
  * sum over visible dwords d at (row, byte_x) of mix64(mix64((row << 32) | byte_x) ^ d) mod 2^64
  * (numpy twin: tiny_mp2v_dec_amd.records.planes_digest) */

@@ -731,10 +731,11 @@ static int plan_batch(mp2vg_ctx_t* c, const mp2vg_picture_t* pics, int32_t npics
         // Measured neutral on c1 (one-stream I launch 0.286 ms either way, profiles/r5/README.md):
         // the skipped stores were already branched over per slice.  (MP2VG_I_TILEFREE=0 in dev
         // builds keeps mode 0.)
-        static const bool tilefree = !dev_env("MP2VG_I_TILEFREE") || atoi(dev_env("MP2VG_I_TILEFREE")) != 0;
+        // (MP2VG_I_TILEFREE=2 in dev builds: every I-only launch, whatever stores tiles, 4:4:4 too)
+        static const int tilefree = !dev_env("MP2VG_I_TILEFREE") ? 1 : atoi(dev_env("MP2VG_I_TILEFREE"));
         int nneed = 0;
         for (int p : lp) nneed += need[p];
-        if (types == 1 && tilefree && c->g.cf != 3 && nneed * 4 <= (int)lp.size()) {
+        if (types == 1 && (tilefree == 2 || (tilefree && c->g.cf != 3 && nneed * 4 <= (int)lp.size()))) {
             l.mcm = 4;
             for (uint32_t k = l.begin; k < l.end; k++) slices[k].reserved = 0;
         }
@@ -1123,6 +1124,12 @@ extern "C" int mp2vg_invalidate_slot(mp2vg_ctx_t* c, int32_t slot) {
 extern "C" int mp2vg_slot_device_ptr(mp2vg_ctx_t* c, int32_t slot, void** dptr) {
     if (!c || !dptr || slot < 0 || slot >= c->nslots) return MP2VG_E_INVALID;
     *dptr = (void*)(uintptr_t)c->fptr[slot];
+    return MP2VG_OK;
+}
+
+extern "C" int mp2vg_sink_device_ptr(mp2vg_ctx_t* c, void** dptr) {
+    if (!c || !dptr || !c->d_sink) return MP2VG_E_INVALID;
+    *dptr = (void*)c->d_sink;
     return MP2VG_OK;
 }
 

@@ -1,8 +1,10 @@
 """Drop-in end to end, repeated, with the native phase trace (dev tool, run on the GPU box): the c2
-bench stream (64 GOPs) decoded 6 times by one mp2v_decoder_c (host frames, 16 threads); prints
-frames/s per run, and MP2VG_TRACE's per-phase lines go to stderr, for telling a slow run's phase.
+bench stream (64 GOPs) decoded 6 times by one mp2v_decoder_c per frame mode (host frames, and
+with `both` also device frames, MP2VG_DECODER_DEVICE_FRAMES; 16 threads), runs of the two modes
+interleaved; prints frames/s per run, and MP2VG_TRACE's per-phase lines go to stderr, for telling
+a slow run's phase.
 
-    MP2VG_TRACE=1 python tools/dropin_trace.py [gops] 2> trace.txt
+    MP2VG_TRACE=1 python tools/dropin_trace.py [gops] [host|device|both] [runs] 2> trace.txt
 """
 import json
 import os
@@ -15,16 +17,20 @@ from tiny_mp2v_dec_amd import records as R  # noqa: E402
 from tiny_mp2v_dec_amd.decoder import decoder_config_t, mp2v_decoder_c  # noqa: E402
 
 gops = int(sys.argv[1]) if len(sys.argv) > 1 else 64
+modes = {"host": [False], "device": [True], "both": [False, True]}[sys.argv[2] if len(sys.argv) > 2 else "host"]
+runs = int(sys.argv[3]) if len(sys.argv) > 3 else 6
 w, h, cf, extra, _ = bench.CONFIGS["c2"]
 es = R.generate_es(width=w, height=h, chroma_format=cf, n_gops=gops, seed=1729, **extra)
 n = [0]
-dec = mp2v_decoder_c(decoder_config_t(w, h, cf, pictures_pool_size=24, num_threads=16),
-                     lambda f: n.__setitem__(0, n[0] + 1))
-for run in range(6):
-    n[0] = 0
-    print(f"=== run {run}", file=sys.stderr, flush=True)
-    t0 = time.perf_counter()
-    dec.decode(es)
-    dt = time.perf_counter() - t0
-    print(json.dumps({"run": run, "frames": n[0], "frames_per_s": round(n[0] / dt, 1)}), flush=True)
-dec.close()
+decs = {m: mp2v_decoder_c(decoder_config_t(w, h, cf, pictures_pool_size=24, num_threads=16, device_frames=m),
+                          lambda f: n.__setitem__(0, n[0] + 1)) for m in modes}
+for run in range(runs):
+    for m in modes:
+        n[0] = 0
+        print(f"=== run {run} {'device' if m else 'host'} frames", file=sys.stderr, flush=True)
+        t0 = time.perf_counter()
+        decs[m].decode(es)
+        dt = time.perf_counter() - t0
+        print(json.dumps({"run": run, "device_frames": m, "frames": n[0], "frames_per_s": round(n[0] / dt, 1)}), flush=True)
+for d in decs.values():
+    d.close()

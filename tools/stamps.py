@@ -35,8 +35,8 @@ def main():
     with R.DeviceContext(w, h, cf, p.npics) as d:
         d.upload(p.pics, p.mbs, p.coefs)
         dp = ctypes.c_void_p()
-        lib().mp2vg_slot_device_ptr(d.h, d.nslots - 1, ctypes.byref(dp))
-        addr = ctypes.c_void_p(dp.value + d.slot_bytes + 2048 + 1024)
+        assert lib().mp2vg_sink_device_ptr(d.h, ctypes.byref(dp)) == 0
+        addr = ctypes.c_void_p(dp.value + 2048 + 1024)  # geo.sink (kSinkOff) + 1024: the stamp sums
         assert hip.hipMemset(addr, 0, 3 * 8 * 8) == 0
         d.decode()
         d.synchronize()
