@@ -411,6 +411,14 @@ def main():
                                   lambda d, t, on_dev: ctx.copy_packed(d, t.data_ptr(), on_dev),
                                   ctx.pw, ctx.ph, gathered, args.gather_gops)
 
+    # this box's shader clock under a VALU load on every SIMD (s_memtime against the 100-MHz
+    # s_memrealtime), measured after the timed region: the per-box record behind the box-to-box
+    # spread of the step (profiles/r6/README.md)
+    import ctypes
+    from tiny_mp2v_dec_amd._lib import lib as _native
+    ghz = ctypes.c_double(0.0)
+    clock_ghz = round(ghz.value, 3) if _native().mp2vg_clock_probe(device, ctypes.byref(ghz)) == 0 else None
+
     traffic = profiled_traffic(args.config, gops)
     frames_total = parsed.npics * world * args.steps
     ms_per_step = elapsed * 1000.0 / args.steps
@@ -459,6 +467,7 @@ def main():
                      "sum_launch_ms_per_step": round(float(np.mean([sum(s) for s in kernel_ms])), 4),
                      "dominant_kernel": dominant, "one_stream_span_ms": round(span1, 4),
                      "per_kernel": per_kernel},
+        "box": {"shader_clock_ghz_valu_load": clock_ghz, "host_cpus_visible": os.cpu_count()},
         "frame_digest_of_digests": int(np.bitwise_xor.reduce(np.concatenate(gathered))),
         "provenance": _build.provenance(),
     }

@@ -206,6 +206,9 @@ int  mp2vg_invalidate_slot(mp2vg_ctx_t* ctx, int32_t slot);
  * decode; from +3072 the per-stage cycle sums of a stamp build, tools/stamps.py).  Never written
  * by callers. */
 int  mp2vg_sink_device_ptr(mp2vg_ctx_t* ctx, void** dptr);
+/* diagnostics: the device's shader clock (GHz) while every SIMD issues VALU for ~1 ms (s_memtime
+ * against the 100-MHz s_memrealtime); bench.py records it per box.  Synchronises the device. */
+int  mp2vg_clock_probe(int32_t device, double* ghz);
 /* 64-bit order-independent digest of each listed slot's visible planes, computed on device:
  * sum over visible dwords d at (row, byte_x) of mix64(mix64((row << 32) | byte_x) ^ d) mod 2^64
  * (numpy twin: tiny_mp2v_dec_amd.records.planes_digest) */

@@ -207,6 +207,14 @@ template <int CF>
 struct ResLayout {
     using F = Fmt<CF>;
     static constexpr int SIZE = 256 + 2 * F::CW * F::CH;
+    // MB stride of the P/B kernels' int16 image: SIZE alone is a multiple of 256 B, so the four
+    // MBs' images alias the same LDS banks (the store pass reads row py of MB k, k = 0..3, in one
+    // instruction); 16 B of padding spread them over the banks.  (The I kernels' byte image keeps
+    // SIZE: its capacity sets their occupancy.)
+#ifndef MP2VG_RES_PAD
+#define MP2VG_RES_PAD 0  // 8 measured neutral (c2 381.5k/381.7k vs 382.6k/380.7k, profiles/r6/README.md)
+#endif
+    static constexpr int MBS = SIZE + MP2VG_RES_PAD;
     __device__ static constexpr int base(int plane) { return plane == 0 ? 0 : 256 + (plane - 1) * F::CW * F::CH; }
     __device__ static constexpr int width(int plane) { return plane == 0 ? 16 : F::CW; }
     __device__ static int pos(int x) { return (x & ~3) | ((x & 1) << 1) | ((x >> 1) & 1); }
@@ -380,7 +388,30 @@ __device__ __forceinline__ void load_row(uint32_t (&d)[NW + 1], __amdgpu_buffer_
 #endif
 constexpr bool kChromaTiles = MP2VG_CHROMA_TILES;  // dev A/B: 0 = chroma taps from the frame rows
 
-template <int CF, int NW, int ABL = 0, bool TL = true>
+// v_mad_u32_u24 with a wave-uniform (SGPR) factor: a * b + c, 24-bit a and b (full 32-bit c)
+__device__ __forceinline__ uint32_t mad24s_asm(uint32_t a, uint32_t b_uniform, uint32_t c) {
+    uint32_t r;
+    asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(r) : "v"(a), "s"(b_uniform), "v"(c));
+    return r;
+}
+
+// Tap issue (round 6, same-box A/B in profiles/r6/README.md):
+// MP2VG_TAP_MAD -- a tap row's tile offset as one 24-bit multiply-add, tile_off(x, y) =
+//   (y >> lr) * (ncol * 128 - 128) + y * RB + xterm (RB = 128 >> lr bytes per tile row, xterm =
+//   (x >> lw) * 128 + (x & (W - 4)) shared by both rows of the tap): -36 fast, +8 slow VALU per B group;
+// MP2VG_ROW2_LOAD -- in the B loop every lane loads its second half-pel row itself (the lane's own
+//   row again without vertical half-pel) instead of taking it from the next-row lane by
+//   ds_bpermute (-16 ds_bpermute and -48 slow VALU per B group, one more full-width load per
+//   direction and pass); the P loop keeps the ds_bpermute (its one direction's TA cost weighs more:
+//   +0.5-1 % on the P launch with ROW2).  Both: B launch -3 %, P+B -1 % (c2).
+#ifndef MP2VG_TAP_MAD
+#define MP2VG_TAP_MAD 1
+#endif
+#ifndef MP2VG_ROW2_LOAD
+#define MP2VG_ROW2_LOAD 1
+#endif
+
+template <int CF, int NW, int ABL = 0, bool TL = true, bool R2 = false>
 __device__ __forceinline__ void tap_issue(Tap<NW>& t, bool use, __amdgpu_buffer_rsrc_t ref, uint32_t plane_off,
                                           uint32_t mvw, int plane, int gx, int py, int phm, int mby_base, bool field,
                                           int fs, int stride, int ph) {
@@ -411,12 +442,20 @@ __device__ __forceinline__ void tap_issue(Tap<NW>& t, bool use, __amdgpu_buffer_
     // byte-exact (unaligned) buffer loads would save two alignbytes per dword but cost twice the
     // texture-address cycles, a net loss (tools/unaligned_check.hip)
     const uint32_t ncol = (uint32_t)stride >> (NW == 4 ? 4 : 3);
+    constexpr int LW = NW == 4 ? 4 : 3, LR = NW == 4 ? 2 : 3;  // log2 tile width (px), rows per tile
+    const uint32_t xterm = ((uint32_t)Xc >> LW) * 128u + ((uint32_t)Xc & (4u * NW - 4u)) + plane_off;
+    const uint32_t pitch_m = ncol * 128u - 128u;  // wave-uniform (issue_pass)
     auto toff = [&](int y) -> uint32_t {
+        if (TL && MP2VG_TAP_MAD)
+            return mad24s_asm((uint32_t)y >> LR, pitch_m, ((uint32_t)y << (7 - LR)) + xterm);
         return TL ? plane_off + tile_off<4 * NW>((uint32_t)Xc, (uint32_t)y, ncol)
                   : plane_off + (uint32_t)(Xc & ~3) + mul24_asm((uint32_t)y, (uint32_t)stride);
     };
     uint32_t o0 = (use && !(ABL & 32)) ? toff(Y0) : kNoTap;
-    uint32_t o1 = (use && hy && edge && !(ABL & 32)) ? toff(Y1) : kNoTap;
+    // second row: only edge lanes load it (the others take it from the next-row lane, tap_rows),
+    // or with MP2VG_ROW2_LOAD every lane (its own row again without vertical half-pel)
+    uint32_t o1 = R2 ? ((use && !(ABL & 32)) ? (hy ? toff(Y1) : o0) : kNoTap)
+                     : ((use && hy && edge && !(ABL & 32)) ? toff(Y1) : kNoTap);
     if (ABL & 2048) {  // dev ablation (timing only): every tap inside a 64-KB window (L1/L2 hits)
         o0 = o0 == kNoTap ? kNoTap : (o0 & 0xFFFFu);
         o1 = o1 == kNoTap ? kNoTap : (o1 & 0xFFFFu);
@@ -471,8 +510,10 @@ __device__ __forceinline__ void predict(Tap<NW>& tf, Tap<NW>& tb, int lane, uint
         for (int d = 0; d < NW; d++) p[d] = tf.a[d] ^ tf.b[d] ^ (MCM == 2 ? tb.a[d] ^ tb.b[d] : 0u);
         return;
     }
-    tap_rows<NW>(tf, lane);
-    if (MCM == 2) tap_rows<NW>(tb, lane);
+    if (!(MP2VG_ROW2_LOAD && MCM == 2)) {  // (ROW2: the B loop's taps loaded both rows)
+        tap_rows<NW>(tf, lane);
+        if (MCM == 2) tap_rows<NW>(tb, lane);
+    }
     const bool uf = tf.ctl & 16, ub = MCM == 2 && (tb.ctl & 16);
     uint32_t pf[NW], pb[NW];
 #pragma unroll
@@ -518,16 +559,19 @@ __device__ __forceinline__ void issue_pass(const LaneRec& L, bool live, int lane
     const int gx = (int)(L.r0 & 0xffff) * pw;
     const int mbyb = (int)(L.r0 >> 16) * phm;
     const int r = field ? (py & 1) : 0;
-    const int stride = gsel(geo.stride, plane);
-    const int ph = gsel(geo.ph, plane);
+    // wave-uniform: a pass is luma (J 0) or chroma, and Cb and Cr share their stride and height
+    // (frame_c layout), so the row pitch stays in SGPRs (lane-selected, it cost readfirstlanes)
+    const int stride = J == 0 ? geo.stride[0] : geo.stride[1];
+    const int ph = J == 0 ? geo.ph[0] : geo.ph[1];
     constexpr bool TL = J == 0 || kChromaTiles;
     const uint32_t off = (TL ? 2u : 1u) * (uint32_t)gsel(geo.plane_off, plane);  // the plane in the tile slot
     const uint32_t mv1 = (MCM == 1 && dir) ? L.mvb : L.mvf;
     const int fsh = 8 + 2 * r + (MCM == 1 ? dir : 0);
-    tap_issue<CF, NW, ABL, TL>(tf, fwd, ref_fwd, off, mv1, plane, gx, py, phm, mbyb, field, (fl >> fsh) & 1, stride, ph);
+    constexpr bool R2 = MP2VG_ROW2_LOAD && MCM == 2;
+    tap_issue<CF, NW, ABL, TL, R2>(tf, fwd, ref_fwd, off, mv1, plane, gx, py, phm, mbyb, field, (fl >> fsh) & 1, stride, ph);
     if (MCM == 2)
-        tap_issue<CF, NW, ABL, TL>(tb, !none && bwd, ref_bwd, off, L.mvb, plane, gx, py, phm, mbyb, field,
-                                   (fl >> (9 + 2 * r)) & 1, stride, ph);
+        tap_issue<CF, NW, ABL, TL, R2>(tb, !none && bwd, ref_bwd, off, L.mvb, plane, gx, py, phm, mbyb, field,
+                                       (fl >> (9 + 2 * r)) & 1, stride, ph);
 }
 
 // frame_c row stores (16 / 8 B).  Nontemporal stores measured c2 -8.5 %, c3 -19 % (round 4).
@@ -588,7 +632,7 @@ __device__ __forceinline__ void store_pass(uint32_t r0, uint32_t r1, bool live, 
 #pragma unroll
     for (int d = 0; d < NW; d++) out[d] = p[d];
     if (cl || cr) {
-        const short* res = s_res_wave + k * RL::SIZE + RL::base(plane) + py * RL::width(plane);
+        const short* res = s_res_wave + k * RL::MBS + RL::base(plane) + py * RL::width(plane);
         uint32_t rv[8];
         const uint4 q0 = *(const uint4*)&res[0];
         rv[0] = q0.x; rv[1] = q0.y; rv[2] = q0.z; rv[3] = q0.w;
@@ -618,7 +662,7 @@ __device__ __forceinline__ void store_pass(uint32_t r0, uint32_t r1, bool live, 
         dst = dst_slot + ((((r0 & 0xffff) + (r0 >> 16) * 128u) * 3u + (uint32_t)J) * 1024u + (uint32_t)lane * 16u) %
                              (uint32_t)(geo.plane_off[1] - 1024);
     if (tiles) {  // the row's pixels for tile_group: over the first half of its (read) int16 residual row
-        uint8_t* img = (uint8_t*)(s_res_wave + k * RL::SIZE + RL::base(plane) + py * RL::width(plane));
+        uint8_t* img = (uint8_t*)(s_res_wave + k * RL::MBS + RL::base(plane) + py * RL::width(plane));
         if (NW == 4)
             *(uint4*)img = make_uint4(out[0], out[1], out[2], out[3]);
         else
@@ -691,7 +735,7 @@ __device__ __forceinline__ void store_pass_put8(uint32_t r0, bool live, int lane
 template <int CF, bool NAT>
 __device__ __forceinline__ const uint8_t* img_row(const uint8_t* img, int k, int plane, int py) {
     using RL = ResLayout<CF>;
-    return &img[(NAT ? 2 : 1) * (k * RL::SIZE + RL::base(plane) + py * RL::width(plane))];
+    return &img[(NAT ? 2 : 1) * (k * (NAT ? RL::MBS : RL::SIZE) + RL::base(plane) + py * RL::width(plane))];
 }
 __device__ __forceinline__ uint32_t unswz(uint32_t v, bool nat) { return nat ? v : __builtin_amdgcn_perm(v, v, 0x03010200u); }
 template <int CF, bool NAT>
@@ -780,6 +824,12 @@ constexpr int kAblCompact = 16 | 32768 | 65536;
 template <int MCM, int ABL>
 constexpr bool compact_layout() { return (MCM == 0 || MCM == 4) && (ABL & ~kAblCompact) == 0; }
 constexpr int lds_sets(int cf, bool c8) { return c8 ? 1 : (cf == 3 ? 2 : 4); }
+// the cross-group IDCT pipeline of the 4:2:0 P/B loops (run_slice_pipe; dev A/B switch)
+#ifndef MP2VG_IDCT_PIPE
+#define MP2VG_IDCT_PIPE 0
+#endif
+template <int CF, int MCM, int ABL>
+constexpr bool pipe_layout() { return MP2VG_IDCT_PIPE && CF == 1 && MCM >= 1 && MCM <= 3 && ABL == 0; }
 template <int CF, int MCM, int ABL>
 constexpr uint32_t slices_per_wg(uint32_t mates) {
     return !compact_layout<MCM, ABL>() && kernel_waves<MCM, ABL>() == 4 && (mates == 2 || mates == 4) &&
@@ -789,22 +839,28 @@ constexpr uint32_t slices_per_wg(uint32_t mates) {
 }
 constexpr int BLKS = 72;
 // C8 = the compact layout of the I kernels (4:4:4: 38.4 KB instead of 53.8 KB per workgroup, so
-// four workgroups share a CU instead of three; 4:2:2 26.0 KB, 4:2:0 19.9 KB)
-template <int CF, bool C8 = false, int NWV = WAVES>
+// four workgroups share a CU instead of three; 4:2:2 26.0 KB, 4:2:0 19.9 KB).  PIPE = the 4:2:0
+// P/B layout of the cross-group IDCT pipeline (run_slice_pipe): two coefficient-block buffers and
+// slot maps per wave (group g's pass 1 beside group g-1's pass 2), in 128-B XOR-swizzled slots so
+// that four workgroups still share a CU (39.6 KB)
+template <int CF, bool C8 = false, int NWV = WAVES, bool PIPE = false>
 struct Lds {
     static constexpr bool COMPACT = C8;
+    static constexpr bool X64 = C8 || PIPE;      // 128-B block slots, 16-B chunk index XOR (slot & 7)
+    static constexpr int NBUF = PIPE ? 2 : 1;    // block buffers (and slot maps) per wave
+    static constexpr bool PIPE_LOOP = PIPE;
     static constexpr int NWAVES = NWV;           // waves per workgroup
     static constexpr int STEP = NWV * G;         // a wave's next group starts STEP MBs later
     static constexpr int MAXS = G * Fmt<CF>::NB;  // coded-block slots per group
     // coef raster -> pass-1 out.  Slots 144 B apart (BLK = 72 shorts): the transposed pass-1
     // writes of the 8 slots in a 32-lane half then hit distinct banks (128 B apart: 8-way
     // conflicts).  C8: slots 128 B apart with the 16-B chunk index XOR (slot & 7), same banks.
-    static constexpr int BLK = C8 ? 64 : BLKS;
-    short blk[NWV][MAXS][BLK];
+    static constexpr int BLK = X64 ? 64 : BLKS;
+    short blk[NWV * NBUF][MAXS][BLK];  // wave w, buffer b: blk[w * NBUF + b]
     // residual images, int16 in ResLayout; C8 (intra only: output = clamp(residual)): the clamped
     // pixels as bytes in the same ResLayout order, half the size
-    short res[NWV][C8 ? G * ResLayout<CF>::SIZE / 2 : G * ResLayout<CF>::SIZE];
-    uint8_t map[NWV][MAXS];                      // slot -> k*16 + b
+    short res[NWV][C8 ? G * ResLayout<CF>::SIZE / 2 : G * ResLayout<CF>::MBS];
+    uint8_t map[NWV * NBUF][MAXS];               // slot -> k*16 + b
     uint32_t dq[NWV][64];                        // (k*16 + b) -> dequant parameters (DqEntry)
     // quantiser matrices and scan (C8: the I kernels' one picture per workgroup; P/B layouts NH
     // sets, one per slice when the workgroup runs several, recon_kernel `mates`; 4:4:4 two, so
@@ -819,13 +875,13 @@ struct Lds {
     uint8_t scan[64 * NH];
     uint8_t Wb[WB && CF != 1 ? Fmt<CF>::NB : 0][64];  // zero-length (clang extension) when unused: no layout change
     // short index of coefficient / pass-1 output idx (0..63) of a slot, relative to the wave's blk
-    __device__ static int bofs(int slot, int idx) { return slot * BLK + (C8 ? (idx ^ ((slot & 7) << 3)) : idx); }
+    __device__ static int bofs(int slot, int idx) { return slot * BLK + (X64 ? (idx ^ ((slot & 7) << 3)) : idx); }
 };
 
 // (MB in group) * 16 + block of coded-block slot `slot`: from the group's slot map, or, in I
 // pictures (every MB intra with every block coded), slot = k * NB + b directly
 template <int MCM, int NB, class LT>
-__device__ __forceinline__ int slot_kb(const LT& L, int wave, int slot) {
+__device__ __forceinline__ int slot_kb(const LT& L, int wave, int slot, int buf = 0) {
     if constexpr (MCM == 0) {
         // slot / NB by a 24-bit multiply and a shift, exact for the slots of a group (< 4 * NB)
         // (a plain division became a quarter-rate v_mul_hi_i32 + v_mad_u64_u32)
@@ -833,7 +889,7 @@ __device__ __forceinline__ int slot_kb(const LT& L, int wave, int slot) {
         const int k = NB == 8 ? slot >> 3 : (int)(__umul24((uint32_t)slot, 43u) >> (NB == 6 ? 8 : 9));
         return (k << 4) | (slot - k * NB);
     } else {
-        return L.map[wave][slot];
+        return L.map[wave * LT::NBUF + buf][slot];
     }
 }
 
@@ -851,7 +907,7 @@ __device__ __forceinline__ uint4 ld16(const lds_uint4_t* p) {
 __device__ __forceinline__ void zero16(lds_uint4_t* p) { *p = u4v{0u, 0u, 0u, 0u}; }
 template <class LT>
 __device__ __forceinline__ void pass1_store(short* bw, int slot, int v, const short2_t (&s)[8]) {
-    if constexpr (LT::COMPACT) {
+    if constexpr (LT::X64) {
         const uint32_t b0 = (uint32_t)(uintptr_t)(lds_short2_t*)(bw + LT::bofs(slot, v));  // chunk 0 ^ (slot & 7)
 #pragma unroll
         for (int x = 0; x < 8; x++) *(lds_short2_t*)(uintptr_t)(b0 ^ (uint32_t)(x << 4)) = s[x];
@@ -871,7 +927,7 @@ typedef __attribute__((address_space(3))) uint16_t lds_u16_t;
 // and pass 2's zeroing (compact layout: chunk 0 XOR 16c, see pass1_store)
 template <class LT>
 __device__ __forceinline__ void slot_chunks(short* bw, int slot, int ca, int cb, lds_uint4_t*& pa, lds_uint4_t*& pb) {
-    if constexpr (LT::COMPACT) {
+    if constexpr (LT::X64) {
         const uint32_t b0 = (uint32_t)(uintptr_t)(lds_short2_t*)(bw + LT::bofs(slot, 0));
         pa = (lds_uint4_t*)(uintptr_t)(b0 ^ (uint32_t)(ca << 4));
         pb = (lds_uint4_t*)(uintptr_t)(b0 ^ (uint32_t)(cb << 4));
@@ -934,7 +990,8 @@ __device__ __forceinline__ int mul24i_asm(int a, int b) {  // v_mul_i32_i24: sig
 // coefficients) needs no table: the slot is k * NB + b, the matrix is the block's (luma for
 // blocks 0-5, mb_decoder.cpp:111-113), the quantiser scale is byte k of qs8.
 template <class LT, bool INTRA_ONLY = false, int NB = 6>
-__device__ __forceinline__ void dequant_word(LT& L, int wave, uint32_t w, uint32_t qs8, bool live = true, int h = 0) {
+__device__ __forceinline__ void dequant_word(LT& L, int wave, uint32_t w, uint32_t qs8, bool live = true, int h = 0,
+                                             int buf = 0) {
     if constexpr (INTRA_ONLY) {
         const uint32_t k = (w >> 26) & 3u, b = (w >> 22) & 15u;
         const int slot = (int)(k * NB + b);
@@ -998,7 +1055,7 @@ __device__ __forceinline__ void dequant_word(LT& L, int wave, uint32_t w, uint32
         v = s1 ? (short)((t1 ^ sign) - sign) : v;
     }
     v = dc ? (short)level : v;  // branch-free: every lane of the word round writes once
-    ((short*)L.blk[wave])[LT::bofs(slot, L.scan[64 * h + i])] = v;  // i = 0 for DC and '1s' words: block position 0
+    ((short*)L.blk[wave * LT::NBUF + buf])[LT::bofs(slot, L.scan[64 * h + i])] = v;  // i = 0 for DC and '1s' words: block position 0
 }
 
 // force the wait for every tap load here (an empty asm reading the registers): a direction
@@ -1020,7 +1077,8 @@ __device__ __forceinline__ void stamp(Stamps& st, int i) {
     if (!(ABL & 16)) return;
     uint64_t t;
     __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    // (the comment names the stage in the assembly: tools/stage_mix.py splits the loop there)
+    asm volatile("s_memtime %0 ; stage stamp %1\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) : "i"(i) : "memory");
     __builtin_amdgcn_sched_barrier(0);
     if (i >= 0) st.acc[i] += t - st.t;
     st.t = t;
@@ -1260,7 +1318,7 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, LT&
                 } else {
                     // row y at a0 + y * step, one add per row (see put8_rows)
                     const uint32_t a0 = (uint32_t)(uintptr_t)(lds_short2_t*)(&L.res[wave][RL::base(plane)]) +
-                                        2u * (mul24_asm((uint32_t)k, (uint32_t)RL::SIZE) + (uint32_t)(y0 * rw + xp));
+                                        2u * (mul24_asm((uint32_t)k, (uint32_t)RL::MBS) + (uint32_t)(y0 * rw + xp));
                     const uint32_t step = 2u * (uint32_t)(ys * rw);
 #pragma unroll
                     for (int y = 0; y < 8; y++) *(lds_short2_t*)(uintptr_t)(a0 + (uint32_t)y * step) = s[y] >> (short)6;
@@ -1372,6 +1430,220 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, LT&
     }
 }
 
+// P/B loops of the 4:2:0 kernels with the IDCT pipelined across groups (MP2VG_IDCT_PIPE, LT::PIPE).
+// A B group codes ~7 blocks: 29 of a round's 64 lanes per IDCT pass, so run_slice spends two
+// rounds (pass 1, pass 2) on ~58 items.  Here iteration g runs group g's pass 1 and group g-1's
+// pass 2 in the same rounds (item slots [0, n1) pass 1 of g, [n1, n1 + n2) pass 2 of g-1: one
+// round whenever the two fit 64 lanes; c2 B groups 1.94 -> 1.35 rounds, P 2.08 -> 1.68), then
+// stores group g-1.  The two passes share one idct_1d (the exact form; pure pass-1 rounds take
+// the folded one); only their loads/parity and stores diverge.  Group g's blocks sit in buffer
+// `par` while g-1's drain from `par ^ 1` (LT::NBUF = 2, slot maps likewise); the prediction of g
+// (computed at the top of iteration g, taps issued one iteration ahead as in run_slice) is held
+// into iteration g+1 for the store.  Order per iteration: predict g | issue luma taps of g+1 |
+// dequant g | rounds | chroma taps of g+1 | store g-1.  One more iteration after the last group
+// drains its pass 2 and store.  Same semantics as run_slice (mb_decoder.cpp:74-155, :166-196,
+// idct_sse2.hpp:23-120), bit-exact.
+template <int CF, int MCM, int ABL, class LT>
+__device__ __forceinline__ void run_slice_pipe(const SliceCtx& c, const Geo& geo, LT& L, int lane, int wave) {
+    static_assert(LT::NBUF == 2 && CF == 1 && (MCM == 1 || MCM == 2), "pipelined P/B loop: 4:2:0, two block buffers");
+    using F = Fmt<CF>;
+    using RL = ResLayout<CF>;
+    constexpr int NB = F::NB;
+    constexpr int NWC = F::CW / 4;
+    const uint32_t STEP = c.step;
+    const uint32_t mb_end = c.mb_end, mb_last = c.mb_end - 1;
+    uint32_t g = c.mb_begin + c.wpos * G;
+    if (g >= mb_end) return;
+    const int kl = lane & 3;
+
+    Tap<4> t0f, t0b;
+    Tap<NWC> t1f, t1b;
+    Group S;
+    constexpr int NCW = 2;
+    uint32_t gr0, gr1, rvN, cw[NCW];
+    bool glive;
+    {
+        const uint32_t rv = rec_load(c.mbrec, g, mb_last, lane);
+        const int ng = (int)min(mb_end - g, (uint32_t)G);
+        glive = kl < ng;
+        const LaneRec R = lane_rec(rv, lane);
+        issue_pass<CF, MCM, 0, 4, ABL>(R, glive, lane, geo, c.ref_fwd, c.ref_bwd, t0f, t0b, c.dir);
+        S = group_state<NB>(rv, ng);
+        gr0 = R.r0;
+        gr1 = R.r1;
+        __builtin_amdgcn_sched_barrier(0);
+        rvN = rec_load(c.mbrec, g + STEP < mb_end ? g + STEP : g, mb_last, lane);
+        prefetch_words<MCM, NCW>(cw, c, S.coef0, S.ncoef, lane);
+        __builtin_amdgcn_sched_barrier(0);
+        issue_pass<CF, MCM, 1, NWC, ABL>(R, glive, lane, geo, c.cref_fwd, c.cref_bwd, t1f, t1b, c.dir);
+        __builtin_amdgcn_sched_barrier(0);
+        // dummy stores: the prologue's VMEM sequence matches the loop's (see run_slice)
+#pragma unroll
+        for (int j = 0; j < Passes<CF>::N; j++) ((uint32_t*)c.wsink)[j * 4] = 0u;
+    }
+
+    // the previous group (g - STEP): its prediction, records, block count and flags
+    uint32_t pp0[4] = {0, 0, 0, 0}, pp1[NWC];
+#pragma unroll
+    for (int d = 0; d < NWC; d++) pp1[d] = 0;
+    uint32_t gp0 = 0, gp1 = 0, sp_fl8 = 0;
+    int sp_n4 = 0;  // pass-2 items of the previous group
+    bool glivep = false, have_prev = false;
+    int par = 0;
+    for (;;) {
+        const bool cur = g < mb_end;  // wave-uniform
+        if (!cur && !have_prev) break;
+        uint32_t p0[4] = {0, 0, 0, 0}, p1[NWC];
+#pragma unroll
+        for (int d = 0; d < NWC; d++) p1[d] = 0;
+        LaneRec R = {0u, 0u, 0u, 0u};
+        Group SN = S;
+        bool gliveN = false;
+        if (cur) {
+            // ---- prediction of g (taps issued one iteration ago) ----
+            touch(t0f), touch(t1f);
+            if (MCM == 2) touch(t0b), touch(t1b);
+            predict<MCM, 4, ABL>(t0f, t0b, lane, p0);
+            predict<MCM, NWC, ABL>(t1f, t1b, lane, p1);
+            // ---- look-ahead: luma taps of g+1, records of g+2 ----
+            const uint32_t gn = g + STEP < mb_end ? g + STEP : g;
+            const int ngN = (int)min(mb_end - gn, (uint32_t)G);
+            gliveN = kl < ngN;
+            R = lane_rec(rvN, lane);
+            issue_pass<CF, MCM, 0, 4, ABL>(R, gliveN, lane, geo, c.ref_fwd, c.ref_bwd, t0f, t0b, c.dir);
+            SN = group_state<NB>(rvN, ngN);
+            __builtin_amdgcn_sched_barrier(0);
+            rvN = rec_load(c.mbrec, g + 2 * STEP < mb_end ? g + 2 * STEP : g, mb_last, lane);
+            // ---- slot map (buffer par) + dequant of g into block buffer par ----
+            const uint32_t e = dq_entry<CF>(S, lane);
+            L.dq[wave][lane] = e;
+            if (e & (1u << 19)) L.map[wave * 2 + par][e & 0xff] = (uint8_t)lane;
+            wave_sync();
+#pragma unroll
+            for (int j = 0; j < NCW; j++)
+                if (64 * j + lane < S.ncoef) dequant_word<LT, false, NB>(L, wave, cw[j], S.qs8, true, c.half, par);
+            if (S.ncoef > 64 * NCW) {
+                constexpr int XW = 2;
+                for (int base = 64 * NCW; base < S.ncoef; base += 64 * XW) {
+                    uint32_t xw[XW];
+#pragma unroll
+                    for (int j = 0; j < XW; j++) {
+                        const int wi = base + 64 * j + lane;
+                        xw[j] = wi < S.ncoef ? ld_rec(&c.coefs[S.coef0 + wi]) : 0u;
+                    }
+#pragma unroll
+                    for (int j = 0; j < XW; j++)
+                        if (base + 64 * j + lane < S.ncoef) dequant_word<LT, false, NB>(L, wave, xw[j], S.qs8, true, c.half, par);
+                }
+                __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): see run_slice
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            prefetch_words<MCM, NCW>(cw, c, SN.coef0, SN.ncoef, lane);
+            __builtin_amdgcn_sched_barrier(0);
+            wave_sync();
+        }
+
+        // ---- IDCT rounds: pass 1 of g (items [0, n1), buffer par) + pass 2 of g-1 ([n1, n1 + n2)) ----
+        const int n1 = cur ? S.nslots * 4 : 0, n2 = have_prev ? sp_n4 : 0;
+        short* const bw1 = (short*)L.blk[wave * 2 + par];
+        short* const bw2 = (short*)L.blk[wave * 2 + (par ^ 1)];
+        for (int base = 0; base < n1 + n2; base += 64) {
+            const int t = base + lane;
+            if (t < n1 + n2) {
+                const bool p1 = t < n1;
+                const int u = p1 ? t : t - n1;
+                const int slot = u >> 2, q = u & 3;
+                const int v = q * 2;                      // pass 1: rows v, v+1
+                const int x = (q & 1) | ((q & 2) << 1);  // pass 2: columns x, x+2 (0, 1, 4, 5)
+                short* const bw = p1 ? bw1 : bw2;
+                lds_uint4_t *pa, *pb;
+                slot_chunks<LT>(bw, slot, p1 ? v : x, p1 ? v + 1 : x + 2, pa, pb);
+                uint4 ra = ld16(pa);
+                uint4 rb = ld16(pb);
+                short2_t sv[8];
+                if (p1) {
+                    // mismatch control (mb_decoder.cpp:150-152; intra DC excluded, :76), as run_slice
+                    const int k = slot_kb<MCM, NB>(L, wave, slot, par) >> 4;
+                    const bool intra = pick8(S.fl8, k) & MP2VG_MB_INTRA;
+                    uint32_t pr = (ra.x ^ ra.y ^ ra.z ^ ra.w ^ rb.x ^ rb.y ^ rb.z ^ rb.w) & 0x00010001u;
+                    if (v == 0 && intra) pr ^= ra.x & 1u;
+                    pr = (pr ^ (pr >> 16)) & 1u;
+                    pr ^= (uint32_t)__builtin_amdgcn_ds_swizzle((int)pr, 0x041F);
+                    pr ^= (uint32_t)__builtin_amdgcn_ds_swizzle((int)pr, 0x081F);
+                    if (v == 6) rb.w ^= (pr ^ 1u) << 16;
+                    sv[0] = __builtin_bit_cast(short2_t, ra.x), sv[1] = __builtin_bit_cast(short2_t, ra.y);
+                    sv[2] = __builtin_bit_cast(short2_t, ra.z), sv[3] = __builtin_bit_cast(short2_t, ra.w);
+                    sv[4] = __builtin_bit_cast(short2_t, rb.x), sv[5] = __builtin_bit_cast(short2_t, rb.y);
+                    sv[6] = __builtin_bit_cast(short2_t, rb.z), sv[7] = __builtin_bit_cast(short2_t, rb.w);
+                } else {
+                    zero16(pa);
+                    zero16(pb);
+                    interleave(ra, rb, sv);
+                }
+                // one transform for both passes: the folded pass-1 form only when the whole
+                // round is pass 1 (wave-uniform), the exact form otherwise (valid for both)
+                if (base + 64 <= n1)
+                    idct_1d<true>(sv);
+                else
+                    idct_1d(sv);
+                if (p1) {
+                    pass1_store<LT>(bw, slot, v, sv);
+                } else {
+                    const int kb = slot_kb<MCM, NB>(L, wave, slot, par ^ 1);
+                    const int k = kb >> 4, bb = kb & 15;
+                    const bool dctf = pick8(sp_fl8, k) & MP2VG_MB_DCT_FIELD;
+                    int plane, x0, y0, ys;
+                    block_origin<CF>(bb, dctf, plane, x0, y0, ys);
+                    const int rw = RL::width(plane);
+                    const int xp = RL::pos(x0 + x);
+                    const uint32_t a0 = (uint32_t)(uintptr_t)(lds_short2_t*)(&L.res[wave][RL::base(plane)]) +
+                                        2u * (mul24_asm((uint32_t)k, (uint32_t)RL::MBS) + (uint32_t)(y0 * rw + xp));
+                    const uint32_t stp = 2u * (uint32_t)(ys * rw);
+#pragma unroll
+                    for (int y = 0; y < 8; y++) *(lds_short2_t*)(uintptr_t)(a0 + (uint32_t)y * stp) = sv[y] >> (short)6;
+                }
+            }
+            wave_sync();
+        }
+        if (cur) {  // chroma taps of g+1
+            __builtin_amdgcn_sched_barrier(0);
+            issue_pass<CF, MCM, 1, NWC, ABL>(R, gliveN, lane, geo, c.cref_fwd, c.cref_bwd, t1f, t1b, c.dir);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+
+        // ---- E. prediction + residual of g-1, one row store per lane ----
+        if (have_prev) {
+            store_pass<CF, 0, 4, ABL>(gp0, gp1, glivep, lane, geo, c.wsink, c.dst_slot, c.dst_rsrc, MCM != 2 && c.tiles, L.res[wave], pp0);
+            store_pass<CF, 1, NWC, ABL>(gp0, gp1, glivep, lane, geo, c.wsink, c.dst_slot, c.dst_rsrc, MCM != 2 && c.tiles, L.res[wave], pp1);
+            if (MCM != 2 && c.tiles) {
+                wave_sync();
+                const uint32_t r00 = (uint32_t)__builtin_amdgcn_readfirstlane((int)gp0);
+                tile_group<CF, true, ABL>(r00 & 0xffff, r00 >> 16, lane, geo, c.wsink, c.dst_tiles, c.tile_rsrc,
+                                          (const uint8_t*)L.res[wave]);
+            }
+            wave_sync();
+        }
+        if (!cur) break;
+        // g becomes the previous group
+#pragma unroll
+        for (int d = 0; d < 4; d++) pp0[d] = p0[d];
+#pragma unroll
+        for (int d = 0; d < NWC; d++) pp1[d] = p1[d];
+        gp0 = gr0;
+        gp1 = gr1;
+        glivep = glive;
+        sp_fl8 = S.fl8;
+        sp_n4 = S.nslots * 4;
+        have_prev = true;
+        par ^= 1;
+        S = SN;
+        gr0 = R.r0;
+        gr1 = R.r1;
+        glive = gliveN;
+        g += STEP;
+    }
+}
+
 // Occupancy targets per kernel from its LDS: 4:2:0 / 4:2:2 P/B workgroups fit 4 per CU (128
 // VGPRs), 4:4:4 P/B 3 (168 VGPRs cost nothing); the compact I kernels fit 4 (4:4:4) or 6 (80 VGPRs)
 template <int CF, int MCM, int ABL = 0>
@@ -1385,7 +1657,7 @@ __global__ __launch_bounds__((64 * kernel_waves<MCM, ABL>())) __attribute__((amd
                                                     const Geo geo,
                                                     const uint32_t slice_base, const uint32_t nslices,
                                                     const uint32_t mates) {
-    using LT = Lds<CF, compact_layout<MCM, ABL>(), kernel_waves<MCM, ABL>()>;
+    using LT = Lds<CF, compact_layout<MCM, ABL>(), kernel_waves<MCM, ABL>(), pipe_layout<CF, MCM, ABL>()>;
     __shared__ __attribute__((aligned(128))) LT L;  // 128-B aligned: pass1_store
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -1420,7 +1692,7 @@ __global__ __launch_bounds__((64 * kernel_waves<MCM, ABL>())) __attribute__((amd
             for (int bb = 0; bb < Fmt<CF>::NB; bb++) L.Wb[bb][lane] = pic->W[bb < 6 ? 0 : 2][lane];
         }
     }
-    for (int i = lane; i < LT::MAXS * LT::BLK / 2; i += 64) ((uint32_t*)L.blk[wave])[i] = 0;
+    for (int i = lane; i < LT::NBUF * LT::MAXS * LT::BLK / 2; i += 64) ((uint32_t*)L.blk[wave * LT::NBUF])[i] = 0;
     __syncthreads();
     if (!have) return;
 
@@ -1457,6 +1729,12 @@ __global__ __launch_bounds__((64 * kernel_waves<MCM, ABL>())) __attribute__((amd
     c.step = (two ? wps : (uint32_t)LT::NWAVES) * G;
     if constexpr (MCM == 4) {
         run_slice<CF, 0, ABL, LT, false>(c, geo, L, lane, wave);
+    } else if constexpr (LT::PIPE_LOOP) {  // 4:2:0 P/B loops with the cross-group IDCT pipeline
+        const int pct = pic->picture_coding_type;
+        if (MCM == 2 || (MCM == 3 && pct == 3 && !one_dir))
+            run_slice_pipe<CF, 2, ABL, LT>(c, geo, L, lane, wave);
+        else
+            run_slice_pipe<CF, 1, ABL, LT>(c, geo, L, lane, wave);
     } else if constexpr (MCM < 3) {
         run_slice<CF, (ABL & 2) ? 0 : MCM, ABL, LT>(c, geo, L, lane, wave);
     } else {  // mixed level: the picture type picks the specialised loop (uniform per workgroup)
@@ -1651,6 +1929,31 @@ hipError_t launch_frame_copy(const FrameCopy& fc, int n, uint64_t bytes, hipStre
     // the next chunk's decode
     dim3 block(256), grid(n < 64 ? 64 / n : 1, n);
     hipLaunchKernelGGL(frame_copy_kernel, grid, block, 0, stream, fc, bytes);
+    return hipGetLastError();
+}
+
+// Shader clock under a VALU load on every SIMD (bench.py's per-box record): each wave runs a chain
+// of dependent-free v_add/v_xor for `iters` iterations between two s_memtime / s_memrealtime
+// pairs (s_memtime counts shader cycles, s_memrealtime a constant 100 MHz); out[0] += cycles,
+// out[1] += 100-MHz ticks, summed over waves.  Read-only timers, vector stores only.
+__global__ void __launch_bounds__(256) clock_probe_kernel(unsigned long long* __restrict__ out, int iters) {
+    uint32_t a = threadIdx.x, b = a * 2654435761u, c2 = a ^ 0x9e3779b9u, d = ~a;
+    uint64_t t0, r0, t1, r1;
+    asm volatile("s_memtime %0\n s_memrealtime %1\n s_waitcnt lgkmcnt(0)" : "=s"(t0), "=s"(r0)::"memory");
+    for (int i = 0; i < iters; i++) {
+        asm volatile("v_add_u32 %0, %0, %1\n v_xor_b32 %1, %1, %2\n v_add_u32 %2, %2, %3\n v_xor_b32 %3, %3, %0"
+                     : "+v"(a), "+v"(b), "+v"(c2), "+v"(d));
+    }
+    asm volatile("s_memtime %0\n s_memrealtime %1\n s_waitcnt lgkmcnt(0)" : "=s"(t1), "=s"(r1)::"memory");
+    if ((a ^ b ^ c2 ^ d) == 0x12345678u) out[2] = 1;  // keeps the chain live
+    if ((threadIdx.x & 63) == 0) {
+        atomicAdd(&out[0], (unsigned long long)(t1 - t0));
+        atomicAdd(&out[1], (unsigned long long)(r1 - r0));
+    }
+}
+
+hipError_t launch_clock_probe(unsigned long long* d_out, int iters, int blocks, hipStream_t stream) {
+    hipLaunchKernelGGL(clock_probe_kernel, dim3(blocks), dim3(256), 0, stream, d_out, iters);
     return hipGetLastError();
 }
 

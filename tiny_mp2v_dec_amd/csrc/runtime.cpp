@@ -21,6 +21,7 @@
 namespace mp2vg {
 hipError_t launch_recon(int cf, int mcm, const KArgs& a, hipStream_t stream);
 hipError_t launch_tile_convert(const KArgs& a, int cf, const int32_t* d_list, int n, int32_t slot0, hipStream_t stream);
+hipError_t launch_clock_probe(unsigned long long* d_out, int iters, int blocks, hipStream_t stream);
 hipError_t launch_digest(const uint64_t* ftab, const int32_t* d_slots, int n,
                          const uint64_t off[3], const int32_t stride[3], const int32_t w[3],
                          const int32_t h[3], unsigned long long* d_out, hipStream_t stream);
@@ -1124,6 +1125,25 @@ extern "C" int mp2vg_invalidate_slot(mp2vg_ctx_t* c, int32_t slot) {
 extern "C" int mp2vg_slot_device_ptr(mp2vg_ctx_t* c, int32_t slot, void** dptr) {
     if (!c || !dptr || slot < 0 || slot >= c->nslots) return MP2VG_E_INVALID;
     *dptr = (void*)(uintptr_t)c->fptr[slot];
+    return MP2VG_OK;
+}
+
+extern "C" int mp2vg_clock_probe(int32_t device, double* ghz) {
+    if (!ghz) return MP2VG_E_INVALID;
+    HIPCHK(hipSetDevice(device));
+    int ncu = 0;
+    HIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device));
+    unsigned long long* d = nullptr;
+    HIPCHK(hipMalloc((void**)&d, 3 * sizeof(unsigned long long)));
+    unsigned long long h[3] = {0, 0, 0};
+    hipError_t e = hipMemset(d, 0, sizeof(h));
+    // 4 waves per SIMD on every CU, ~1 ms of VALU issue
+    if (e == hipSuccess) e = launch_clock_probe(d, 1 << 15, ncu * 4, nullptr);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = hipMemcpy(h, d, sizeof(h), hipMemcpyDeviceToHost);
+    hipFree(d);
+    if (e != hipSuccess || h[1] == 0) return MP2VG_E_HIP;
+    *ghz = (double)h[0] / (double)h[1] * 0.1;
     return MP2VG_OK;
 }
 
