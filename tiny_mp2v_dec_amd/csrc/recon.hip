@@ -824,12 +824,6 @@ constexpr int kAblCompact = 16 | 32768 | 65536;
 template <int MCM, int ABL>
 constexpr bool compact_layout() { return (MCM == 0 || MCM == 4) && (ABL & ~kAblCompact) == 0; }
 constexpr int lds_sets(int cf, bool c8) { return c8 ? 1 : (cf == 3 ? 2 : 4); }
-// the cross-group IDCT pipeline of the 4:2:0 P/B loops (run_slice_pipe; dev A/B switch)
-#ifndef MP2VG_IDCT_PIPE
-#define MP2VG_IDCT_PIPE 0
-#endif
-template <int CF, int MCM, int ABL>
-constexpr bool pipe_layout() { return MP2VG_IDCT_PIPE && CF == 1 && MCM >= 1 && MCM <= 3 && ABL == 0; }
 template <int CF, int MCM, int ABL>
 constexpr uint32_t slices_per_wg(uint32_t mates) {
     return !compact_layout<MCM, ABL>() && kernel_waves<MCM, ABL>() == 4 && (mates == 2 || mates == 4) &&
@@ -839,16 +833,14 @@ constexpr uint32_t slices_per_wg(uint32_t mates) {
 }
 constexpr int BLKS = 72;
 // C8 = the compact layout of the I kernels (4:4:4: 38.4 KB instead of 53.8 KB per workgroup, so
-// four workgroups share a CU instead of three; 4:2:2 26.0 KB, 4:2:0 19.9 KB).  PIPE = the 4:2:0
-// P/B layout of the cross-group IDCT pipeline (run_slice_pipe): two coefficient-block buffers and
-// slot maps per wave (group g's pass 1 beside group g-1's pass 2), in 128-B XOR-swizzled slots so
-// that four workgroups still share a CU (39.6 KB)
-template <int CF, bool C8 = false, int NWV = WAVES, bool PIPE = false>
+// four workgroups share a CU instead of three; 4:2:2 26.0 KB, 4:2:0 19.9 KB).  (A double-buffered
+// P/B layout for a cross-group IDCT pipeline -- pass 1 of group g beside pass 2 of g-1 in shared
+// rounds -- was built and measured -7.5 % on c2, profiles/r6/README.md; commit d02a2a6 has it.)
+template <int CF, bool C8 = false, int NWV = WAVES>
 struct Lds {
     static constexpr bool COMPACT = C8;
-    static constexpr bool X64 = C8 || PIPE;      // 128-B block slots, 16-B chunk index XOR (slot & 7)
-    static constexpr int NBUF = PIPE ? 2 : 1;    // block buffers (and slot maps) per wave
-    static constexpr bool PIPE_LOOP = PIPE;
+    static constexpr bool X64 = C8;              // 128-B block slots, 16-B chunk index XOR (slot & 7)
+    static constexpr int NBUF = 1;               // block buffers (and slot maps) per wave
     static constexpr int NWAVES = NWV;           // waves per workgroup
     static constexpr int STEP = NWV * G;         // a wave's next group starts STEP MBs later
     static constexpr int MAXS = G * Fmt<CF>::NB;  // coded-block slots per group
@@ -1430,220 +1422,6 @@ __device__ __forceinline__ void run_slice(const SliceCtx& c, const Geo& geo, LT&
     }
 }
 
-// P/B loops of the 4:2:0 kernels with the IDCT pipelined across groups (MP2VG_IDCT_PIPE, LT::PIPE).
-// A B group codes ~7 blocks: 29 of a round's 64 lanes per IDCT pass, so run_slice spends two
-// rounds (pass 1, pass 2) on ~58 items.  Here iteration g runs group g's pass 1 and group g-1's
-// pass 2 in the same rounds (item slots [0, n1) pass 1 of g, [n1, n1 + n2) pass 2 of g-1: one
-// round whenever the two fit 64 lanes; c2 B groups 1.94 -> 1.35 rounds, P 2.08 -> 1.68), then
-// stores group g-1.  The two passes share one idct_1d (the exact form; pure pass-1 rounds take
-// the folded one); only their loads/parity and stores diverge.  Group g's blocks sit in buffer
-// `par` while g-1's drain from `par ^ 1` (LT::NBUF = 2, slot maps likewise); the prediction of g
-// (computed at the top of iteration g, taps issued one iteration ahead as in run_slice) is held
-// into iteration g+1 for the store.  Order per iteration: predict g | issue luma taps of g+1 |
-// dequant g | rounds | chroma taps of g+1 | store g-1.  One more iteration after the last group
-// drains its pass 2 and store.  Same semantics as run_slice (mb_decoder.cpp:74-155, :166-196,
-// idct_sse2.hpp:23-120), bit-exact.
-template <int CF, int MCM, int ABL, class LT>
-__device__ __forceinline__ void run_slice_pipe(const SliceCtx& c, const Geo& geo, LT& L, int lane, int wave) {
-    static_assert(LT::NBUF == 2 && CF == 1 && (MCM == 1 || MCM == 2), "pipelined P/B loop: 4:2:0, two block buffers");
-    using F = Fmt<CF>;
-    using RL = ResLayout<CF>;
-    constexpr int NB = F::NB;
-    constexpr int NWC = F::CW / 4;
-    const uint32_t STEP = c.step;
-    const uint32_t mb_end = c.mb_end, mb_last = c.mb_end - 1;
-    uint32_t g = c.mb_begin + c.wpos * G;
-    if (g >= mb_end) return;
-    const int kl = lane & 3;
-
-    Tap<4> t0f, t0b;
-    Tap<NWC> t1f, t1b;
-    Group S;
-    constexpr int NCW = 2;
-    uint32_t gr0, gr1, rvN, cw[NCW];
-    bool glive;
-    {
-        const uint32_t rv = rec_load(c.mbrec, g, mb_last, lane);
-        const int ng = (int)min(mb_end - g, (uint32_t)G);
-        glive = kl < ng;
-        const LaneRec R = lane_rec(rv, lane);
-        issue_pass<CF, MCM, 0, 4, ABL>(R, glive, lane, geo, c.ref_fwd, c.ref_bwd, t0f, t0b, c.dir);
-        S = group_state<NB>(rv, ng);
-        gr0 = R.r0;
-        gr1 = R.r1;
-        __builtin_amdgcn_sched_barrier(0);
-        rvN = rec_load(c.mbrec, g + STEP < mb_end ? g + STEP : g, mb_last, lane);
-        prefetch_words<MCM, NCW>(cw, c, S.coef0, S.ncoef, lane);
-        __builtin_amdgcn_sched_barrier(0);
-        issue_pass<CF, MCM, 1, NWC, ABL>(R, glive, lane, geo, c.cref_fwd, c.cref_bwd, t1f, t1b, c.dir);
-        __builtin_amdgcn_sched_barrier(0);
-        // dummy stores: the prologue's VMEM sequence matches the loop's (see run_slice)
-#pragma unroll
-        for (int j = 0; j < Passes<CF>::N; j++) ((uint32_t*)c.wsink)[j * 4] = 0u;
-    }
-
-    // the previous group (g - STEP): its prediction, records, block count and flags
-    uint32_t pp0[4] = {0, 0, 0, 0}, pp1[NWC];
-#pragma unroll
-    for (int d = 0; d < NWC; d++) pp1[d] = 0;
-    uint32_t gp0 = 0, gp1 = 0, sp_fl8 = 0;
-    int sp_n4 = 0;  // pass-2 items of the previous group
-    bool glivep = false, have_prev = false;
-    int par = 0;
-    for (;;) {
-        const bool cur = g < mb_end;  // wave-uniform
-        if (!cur && !have_prev) break;
-        uint32_t p0[4] = {0, 0, 0, 0}, p1[NWC];
-#pragma unroll
-        for (int d = 0; d < NWC; d++) p1[d] = 0;
-        LaneRec R = {0u, 0u, 0u, 0u};
-        Group SN = S;
-        bool gliveN = false;
-        if (cur) {
-            // ---- prediction of g (taps issued one iteration ago) ----
-            touch(t0f), touch(t1f);
-            if (MCM == 2) touch(t0b), touch(t1b);
-            predict<MCM, 4, ABL>(t0f, t0b, lane, p0);
-            predict<MCM, NWC, ABL>(t1f, t1b, lane, p1);
-            // ---- look-ahead: luma taps of g+1, records of g+2 ----
-            const uint32_t gn = g + STEP < mb_end ? g + STEP : g;
-            const int ngN = (int)min(mb_end - gn, (uint32_t)G);
-            gliveN = kl < ngN;
-            R = lane_rec(rvN, lane);
-            issue_pass<CF, MCM, 0, 4, ABL>(R, gliveN, lane, geo, c.ref_fwd, c.ref_bwd, t0f, t0b, c.dir);
-            SN = group_state<NB>(rvN, ngN);
-            __builtin_amdgcn_sched_barrier(0);
-            rvN = rec_load(c.mbrec, g + 2 * STEP < mb_end ? g + 2 * STEP : g, mb_last, lane);
-            // ---- slot map (buffer par) + dequant of g into block buffer par ----
-            const uint32_t e = dq_entry<CF>(S, lane);
-            L.dq[wave][lane] = e;
-            if (e & (1u << 19)) L.map[wave * 2 + par][e & 0xff] = (uint8_t)lane;
-            wave_sync();
-#pragma unroll
-            for (int j = 0; j < NCW; j++)
-                if (64 * j + lane < S.ncoef) dequant_word<LT, false, NB>(L, wave, cw[j], S.qs8, true, c.half, par);
-            if (S.ncoef > 64 * NCW) {
-                constexpr int XW = 2;
-                for (int base = 64 * NCW; base < S.ncoef; base += 64 * XW) {
-                    uint32_t xw[XW];
-#pragma unroll
-                    for (int j = 0; j < XW; j++) {
-                        const int wi = base + 64 * j + lane;
-                        xw[j] = wi < S.ncoef ? ld_rec(&c.coefs[S.coef0 + wi]) : 0u;
-                    }
-#pragma unroll
-                    for (int j = 0; j < XW; j++)
-                        if (base + 64 * j + lane < S.ncoef) dequant_word<LT, false, NB>(L, wave, xw[j], S.qs8, true, c.half, par);
-                }
-                __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): see run_slice
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            prefetch_words<MCM, NCW>(cw, c, SN.coef0, SN.ncoef, lane);
-            __builtin_amdgcn_sched_barrier(0);
-            wave_sync();
-        }
-
-        // ---- IDCT rounds: pass 1 of g (items [0, n1), buffer par) + pass 2 of g-1 ([n1, n1 + n2)) ----
-        const int n1 = cur ? S.nslots * 4 : 0, n2 = have_prev ? sp_n4 : 0;
-        short* const bw1 = (short*)L.blk[wave * 2 + par];
-        short* const bw2 = (short*)L.blk[wave * 2 + (par ^ 1)];
-        for (int base = 0; base < n1 + n2; base += 64) {
-            const int t = base + lane;
-            if (t < n1 + n2) {
-                const bool p1 = t < n1;
-                const int u = p1 ? t : t - n1;
-                const int slot = u >> 2, q = u & 3;
-                const int v = q * 2;                      // pass 1: rows v, v+1
-                const int x = (q & 1) | ((q & 2) << 1);  // pass 2: columns x, x+2 (0, 1, 4, 5)
-                short* const bw = p1 ? bw1 : bw2;
-                lds_uint4_t *pa, *pb;
-                slot_chunks<LT>(bw, slot, p1 ? v : x, p1 ? v + 1 : x + 2, pa, pb);
-                uint4 ra = ld16(pa);
-                uint4 rb = ld16(pb);
-                short2_t sv[8];
-                if (p1) {
-                    // mismatch control (mb_decoder.cpp:150-152; intra DC excluded, :76), as run_slice
-                    const int k = slot_kb<MCM, NB>(L, wave, slot, par) >> 4;
-                    const bool intra = pick8(S.fl8, k) & MP2VG_MB_INTRA;
-                    uint32_t pr = (ra.x ^ ra.y ^ ra.z ^ ra.w ^ rb.x ^ rb.y ^ rb.z ^ rb.w) & 0x00010001u;
-                    if (v == 0 && intra) pr ^= ra.x & 1u;
-                    pr = (pr ^ (pr >> 16)) & 1u;
-                    pr ^= (uint32_t)__builtin_amdgcn_ds_swizzle((int)pr, 0x041F);
-                    pr ^= (uint32_t)__builtin_amdgcn_ds_swizzle((int)pr, 0x081F);
-                    if (v == 6) rb.w ^= (pr ^ 1u) << 16;
-                    sv[0] = __builtin_bit_cast(short2_t, ra.x), sv[1] = __builtin_bit_cast(short2_t, ra.y);
-                    sv[2] = __builtin_bit_cast(short2_t, ra.z), sv[3] = __builtin_bit_cast(short2_t, ra.w);
-                    sv[4] = __builtin_bit_cast(short2_t, rb.x), sv[5] = __builtin_bit_cast(short2_t, rb.y);
-                    sv[6] = __builtin_bit_cast(short2_t, rb.z), sv[7] = __builtin_bit_cast(short2_t, rb.w);
-                } else {
-                    zero16(pa);
-                    zero16(pb);
-                    interleave(ra, rb, sv);
-                }
-                // one transform for both passes: the folded pass-1 form only when the whole
-                // round is pass 1 (wave-uniform), the exact form otherwise (valid for both)
-                if (base + 64 <= n1)
-                    idct_1d<true>(sv);
-                else
-                    idct_1d(sv);
-                if (p1) {
-                    pass1_store<LT>(bw, slot, v, sv);
-                } else {
-                    const int kb = slot_kb<MCM, NB>(L, wave, slot, par ^ 1);
-                    const int k = kb >> 4, bb = kb & 15;
-                    const bool dctf = pick8(sp_fl8, k) & MP2VG_MB_DCT_FIELD;
-                    int plane, x0, y0, ys;
-                    block_origin<CF>(bb, dctf, plane, x0, y0, ys);
-                    const int rw = RL::width(plane);
-                    const int xp = RL::pos(x0 + x);
-                    const uint32_t a0 = (uint32_t)(uintptr_t)(lds_short2_t*)(&L.res[wave][RL::base(plane)]) +
-                                        2u * (mul24_asm((uint32_t)k, (uint32_t)RL::MBS) + (uint32_t)(y0 * rw + xp));
-                    const uint32_t stp = 2u * (uint32_t)(ys * rw);
-#pragma unroll
-                    for (int y = 0; y < 8; y++) *(lds_short2_t*)(uintptr_t)(a0 + (uint32_t)y * stp) = sv[y] >> (short)6;
-                }
-            }
-            wave_sync();
-        }
-        if (cur) {  // chroma taps of g+1
-            __builtin_amdgcn_sched_barrier(0);
-            issue_pass<CF, MCM, 1, NWC, ABL>(R, gliveN, lane, geo, c.cref_fwd, c.cref_bwd, t1f, t1b, c.dir);
-            __builtin_amdgcn_sched_barrier(0);
-        }
-
-        // ---- E. prediction + residual of g-1, one row store per lane ----
-        if (have_prev) {
-            store_pass<CF, 0, 4, ABL>(gp0, gp1, glivep, lane, geo, c.wsink, c.dst_slot, c.dst_rsrc, MCM != 2 && c.tiles, L.res[wave], pp0);
-            store_pass<CF, 1, NWC, ABL>(gp0, gp1, glivep, lane, geo, c.wsink, c.dst_slot, c.dst_rsrc, MCM != 2 && c.tiles, L.res[wave], pp1);
-            if (MCM != 2 && c.tiles) {
-                wave_sync();
-                const uint32_t r00 = (uint32_t)__builtin_amdgcn_readfirstlane((int)gp0);
-                tile_group<CF, true, ABL>(r00 & 0xffff, r00 >> 16, lane, geo, c.wsink, c.dst_tiles, c.tile_rsrc,
-                                          (const uint8_t*)L.res[wave]);
-            }
-            wave_sync();
-        }
-        if (!cur) break;
-        // g becomes the previous group
-#pragma unroll
-        for (int d = 0; d < 4; d++) pp0[d] = p0[d];
-#pragma unroll
-        for (int d = 0; d < NWC; d++) pp1[d] = p1[d];
-        gp0 = gr0;
-        gp1 = gr1;
-        glivep = glive;
-        sp_fl8 = S.fl8;
-        sp_n4 = S.nslots * 4;
-        have_prev = true;
-        par ^= 1;
-        S = SN;
-        gr0 = R.r0;
-        gr1 = R.r1;
-        glive = gliveN;
-        g += STEP;
-    }
-}
-
 // Occupancy targets per kernel from its LDS: 4:2:0 / 4:2:2 P/B workgroups fit 4 per CU (128
 // VGPRs), 4:4:4 P/B 3 (168 VGPRs cost nothing); the compact I kernels fit 4 (4:4:4) or 6 (80 VGPRs)
 template <int CF, int MCM, int ABL = 0>
@@ -1657,7 +1435,7 @@ __global__ __launch_bounds__((64 * kernel_waves<MCM, ABL>())) __attribute__((amd
                                                     const Geo geo,
                                                     const uint32_t slice_base, const uint32_t nslices,
                                                     const uint32_t mates) {
-    using LT = Lds<CF, compact_layout<MCM, ABL>(), kernel_waves<MCM, ABL>(), pipe_layout<CF, MCM, ABL>()>;
+    using LT = Lds<CF, compact_layout<MCM, ABL>(), kernel_waves<MCM, ABL>()>;
     __shared__ __attribute__((aligned(128))) LT L;  // 128-B aligned: pass1_store
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -1729,12 +1507,6 @@ __global__ __launch_bounds__((64 * kernel_waves<MCM, ABL>())) __attribute__((amd
     c.step = (two ? wps : (uint32_t)LT::NWAVES) * G;
     if constexpr (MCM == 4) {
         run_slice<CF, 0, ABL, LT, false>(c, geo, L, lane, wave);
-    } else if constexpr (LT::PIPE_LOOP) {  // 4:2:0 P/B loops with the cross-group IDCT pipeline
-        const int pct = pic->picture_coding_type;
-        if (MCM == 2 || (MCM == 3 && pct == 3 && !one_dir))
-            run_slice_pipe<CF, 2, ABL, LT>(c, geo, L, lane, wave);
-        else
-            run_slice_pipe<CF, 1, ABL, LT>(c, geo, L, lane, wave);
     } else if constexpr (MCM < 3) {
         run_slice<CF, (ABL & 2) ? 0 : MCM, ABL, LT>(c, geo, L, lane, wave);
     } else {  // mixed level: the picture type picks the specialised loop (uniform per workgroup)
