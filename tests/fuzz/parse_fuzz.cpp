@@ -32,6 +32,7 @@ hipError_t launch_digest(const uint64_t*, const int32_t*, int, const uint64_t*, 
                          const int32_t*, const int32_t*, unsigned long long*, hipStream_t) {
     return hipErrorInvalidValue;
 }
+hipError_t launch_clock_probe(unsigned long long*, int, int, hipStream_t) { return hipErrorInvalidValue; }
 }  // namespace mp2vg
 static long g_valid = 0, g_invalid = 0;
 

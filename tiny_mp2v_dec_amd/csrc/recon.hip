@@ -196,6 +196,10 @@ constexpr int G = 4;               // macroblocks per wave group
 #ifndef MP2VG_I_WAVES
 #define MP2VG_I_WAVES 4
 #endif
+// I kernels: the (MB, block) -> block address table of the intra dequant (Lds::kbtab; dev A/B)
+#ifndef MP2VG_I_KBTAB
+#define MP2VG_I_KBTAB 1
+#endif
 template <int MCM, int ABL>
 constexpr int kernel_waves() { return (MCM == 0 || MCM == 4) && ABL == 0 ? MP2VG_I_WAVES : WAVES; }
 
@@ -866,6 +870,12 @@ struct Lds {
     static constexpr bool WB = C8;
     uint8_t scan[64 * NH];
     uint8_t Wb[WB && CF != 1 ? Fmt<CF>::NB : 0][64];  // zero-length (clang extension) when unused: no layout change
+    // I kernels (MP2VG_I_KBTAB): per coefficient word's (MB in group k, block b) = bits 22-27, the
+    // block's byte address in the wave's blocks with its XOR chunk base, slot * 128 | (slot & 7) * 16
+    // (bits 0-15), and k * 8, the bit offset of MB k's quantiser scale in qs8 (bits 16-20): one LDS
+    // read in place of the slot arithmetic (bfe, bfe, mad, three shifts, bitop3, add3) per word
+    // round.  Last in the layout: c5 is sensitive to where the small tables above sit.
+    uint32_t kbtab[WB ? 64 : 0];
     // short index of coefficient / pass-1 output idx (0..63) of a slot, relative to the wave's blk
     __device__ static int bofs(int slot, int idx) { return slot * BLK + (X64 ? (idx ^ ((slot & 7) << 3)) : idx); }
 };
@@ -993,7 +1003,10 @@ __device__ __forceinline__ void dequant_word(LT& L, int wave, uint32_t w, uint32
         // so W[0][i] directly: one 64-B table, no bank conflicts between block rows
         const int Wi = NB == 6 ? L.W[4 * h][i]
                                : (LT::WB ? ((const uint8_t*)L.Wb)[(w >> 16) & 0x3ffu] : L.W[4 * h + (b < 6 ? 0 : 2)][i]);
-        const uint32_t wq = __umul24((uint32_t)Wi, pick8(qs8, (int)k));
+        uint32_t kb = 0;  // the (k, b) table entry (MP2VG_I_KBTAB)
+        if constexpr (LT::WB && MP2VG_I_KBTAB) kb = L.kbtab[(w >> 22) & 63u];
+        const uint32_t qsk = (LT::WB && MP2VG_I_KBTAB) ? __builtin_amdgcn_ubfe(qs8, kb >> 16, 8) : pick8(qs8, (int)k);
+        const uint32_t wq = __umul24((uint32_t)Wi, qsk);
         // (|level| * W * qs) >> 4 with the sign applied after the shift (truncation toward zero):
         // the signed product, biased by 15 when negative, then an arithmetic shift
         const int p = mul24i_asm(level, (int)wq);
@@ -1010,8 +1023,10 @@ __device__ __forceinline__ void dequant_word(LT& L, int wave, uint32_t w, uint32
         // residual image instead, which IDCT pass 2 rewrites before the store pass reads it
         if constexpr (LT::WB) {
             // byte address: slot * 128 + ((slot & 7) * 16 XOR doubled scan position)
-            const uint32_t a = (uint32_t)(uintptr_t)(lds_short2_t*)L.blk[wave] + ((uint32_t)slot << 7) +
-                               ((((uint32_t)slot << 4) & 0x70u) ^ (uint32_t)L.scan[64 * h + i]);
+            const uint32_t a = MP2VG_I_KBTAB
+                                   ? (uint32_t)(uintptr_t)(lds_short2_t*)L.blk[wave] + ((kb & 0xffffu) ^ (uint32_t)L.scan[64 * h + i])
+                                   : (uint32_t)(uintptr_t)(lds_short2_t*)L.blk[wave] + ((uint32_t)slot << 7) +
+                                         ((((uint32_t)slot << 4) & 0x70u) ^ (uint32_t)L.scan[64 * h + i]);
             const uint32_t d = (uint32_t)(uintptr_t)(lds_short2_t*)L.res[wave];
             *(__attribute__((address_space(3))) short*)(uintptr_t)(live ? a : d) = o;
         } else {
@@ -1465,6 +1480,11 @@ __global__ __launch_bounds__((64 * kernel_waves<MCM, ABL>())) __attribute__((amd
         const int r = c_scan_raster[alt][lane];
         const int pos = (r >> 4) * 16 + (r & 7) * 2 + ((r >> 3) & 1);
         L.scan[64 * half + lane] = (uint8_t)(LT::WB ? 2 * pos : pos);
+        if constexpr (LT::WB && MP2VG_I_KBTAB) {
+            const int k = lane >> 4, bb = lane & 15;
+            const uint32_t slot = (uint32_t)(k * Fmt<CF>::NB + (bb < Fmt<CF>::NB ? bb : 0));
+            L.kbtab[lane] = ((slot << 7) | ((slot << 4) & 0x70u)) | ((uint32_t)k * 8u << 16);
+        }
         if constexpr (LT::WB && CF != 1) {
 #pragma unroll
             for (int bb = 0; bb < Fmt<CF>::NB; bb++) L.Wb[bb][lane] = pic->W[bb < 6 ? 0 : 2][lane];
