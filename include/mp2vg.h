@@ -209,6 +209,14 @@ int  mp2vg_sink_device_ptr(mp2vg_ctx_t* ctx, void** dptr);
 /* diagnostics: the device's shader clock (GHz) while every SIMD issues VALU for ~1 ms (s_memtime
  * against the 100-MHz s_memrealtime); bench.py records it per box.  Synchronises the device. */
 int  mp2vg_clock_probe(int32_t device, double* ghz);
+/* diagnostics (pool placement, tools/placement.py): per pool block (frames and tiles of 16 slots
+ * each, in allocation order: frames, tiles, frames, ...) the HBM rate in GB/s of `reps` sweeps
+ * that load every 16-B word and, with rw = 1, store it back unchanged.  gbps[i] for the first
+ * `max` blocks; *nblocks = the pool's block count.  rw = 2: one rate (gbps[0], *nblocks = 1) for
+ * 1-KB reads at random slots and offsets over the whole pool; rw = 3: the same with many slots read
+ * at one offset at a time; rw = 4: per block, random 1-KB reads inside the block.  Synchronises
+ * the context; contents kept. */
+int  mp2vg_pool_probe(mp2vg_ctx_t* ctx, int32_t rw, int32_t reps, double* gbps, int32_t max, int32_t* nblocks);
 /* 64-bit order-independent digest of each listed slot's visible planes, computed on device:
  * sum over visible dwords d at (row, byte_x) of mix64(mix64((row << 32) | byte_x) ^ d) mod 2^64
  * (numpy twin: tiny_mp2v_dec_amd.records.planes_digest) */

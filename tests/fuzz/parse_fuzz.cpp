@@ -33,6 +33,11 @@ hipError_t launch_digest(const uint64_t*, const int32_t*, int, const uint64_t*, 
     return hipErrorInvalidValue;
 }
 hipError_t launch_clock_probe(unsigned long long*, int, int, hipStream_t) { return hipErrorInvalidValue; }
+hipError_t launch_block_probe(void*, size_t, int, int, void*, hipStream_t) { return hipErrorInvalidValue; }
+hipError_t launch_block_random(const void*, size_t, int, int, void*, hipStream_t) { return hipErrorInvalidValue; }
+hipError_t launch_pool_scatter(const uint64_t*, int, uint32_t, uint32_t, int, int, int, void*, hipStream_t) {
+    return hipErrorInvalidValue;
+}
 }  // namespace mp2vg
 static long g_valid = 0, g_invalid = 0;
 

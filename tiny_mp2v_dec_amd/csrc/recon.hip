@@ -407,12 +407,13 @@ __device__ __forceinline__ uint32_t mad24s_asm(uint32_t a, uint32_t b_uniform, u
 //   row again without vertical half-pel) instead of taking it from the next-row lane by
 //   ds_bpermute (-16 ds_bpermute and -48 slow VALU per B group, one more full-width load per
 //   direction and pass); the P loop keeps the ds_bpermute (its one direction's TA cost weighs more:
-//   +0.5-1 % on the P launch with ROW2).  Both: B launch -3 %, P+B -1 % (c2).
+//   +0.5-1 % on the P launch with ROW2).  Both: B launch -3 %, P+B -1 % (c2, one stream), but the
+//   two-stream step was neutral or slower on 2 of 3 boxes (profiles/r6/README.md §2): off by default.
 #ifndef MP2VG_TAP_MAD
 #define MP2VG_TAP_MAD 1
 #endif
 #ifndef MP2VG_ROW2_LOAD
-#define MP2VG_ROW2_LOAD 1
+#define MP2VG_ROW2_LOAD 0
 #endif
 
 template <int CF, int NW, int ABL = 0, bool TL = true, bool R2 = false>
@@ -1746,6 +1747,97 @@ __global__ void __launch_bounds__(256) clock_probe_kernel(unsigned long long* __
 
 hipError_t launch_clock_probe(unsigned long long* d_out, int iters, int blocks, hipStream_t stream) {
     hipLaunchKernelGGL(clock_probe_kernel, dim3(blocks), dim3(256), 0, stream, d_out, iters);
+    return hipGetLastError();
+}
+
+// Pool-placement probe over one pool block, contents kept: every 16-B word is loaded and (rw)
+// stored back xor `zero` (a runtime 0, so the store is not folded away).  Read-only sweeps fold the
+// words into one store per lane to the sink only when the fold equals `zero`'s complement.
+template <bool RW>
+__global__ void __launch_bounds__(256) block_probe_kernel(u4v* __restrict__ p, size_t n, uint32_t zero, int reps,
+                                                          u4v* __restrict__ sink) {
+    u4v acc = {0, 0, 0, 0};
+    for (int r = 0; r < reps; r++)
+        for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+            u4v v = p[i];
+            if (RW) {
+                v.x ^= zero;
+                p[i] = v;
+            } else {
+                acc ^= v;
+            }
+        }
+    if (!RW && (acc.x ^ acc.y ^ acc.z ^ acc.w) == ~zero) sink[threadIdx.x] = acc;
+}
+
+// Pool-placement probe over the whole pool: every wave reads `iters` 1-KB runs (16 B per lane).
+// LOCK = false: each run in a random slot (frame or tile), at a random 1-KB offset (a page-walk /
+// TLB-reach probe); true: wave w reads slot w % nslots, and run i of every wave sits at the same
+// offset i * 4 KB in its slot (many pictures at one offset at once: the decode's access shape).
+template <bool LOCK>
+__global__ void __launch_bounds__(256) pool_scatter_kernel(const uint64_t* __restrict__ tab, int nslots,
+                                                           uint32_t fkb, uint32_t tkb, int iters,
+                                                           u4v* __restrict__ sink, uint32_t zero) {
+    const uint32_t wave = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    u4v acc = {0, 0, 0, 0};
+    uint32_t h = wave * 2654435761u + 12345u;
+    for (int i = 0; i < iters; i++) {
+        uint32_t slot, tile, kb;
+        if (LOCK) {
+            slot = wave % nslots;
+            tile = wave / nslots & 1;
+            kb = (uint32_t)i * 4 % (tile ? tkb : fkb);
+        } else {
+            h ^= h << 13, h ^= h >> 17, h ^= h << 5;
+            slot = h % nslots;
+            tile = h >> 31;
+            const uint32_t g = h * 0x9e3779b1u;
+            kb = (g >> 8) % (tile ? tkb : fkb);
+        }
+        const u4v* p = (const u4v*)(tab[tile * nslots + slot] + (uint64_t)kb * 1024) + lane;
+        acc ^= *p;
+    }
+    if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == ~zero) sink[threadIdx.x] = acc;
+}
+
+// Random 1-KB reads inside one pool block (its pages only): a block mapped in small fragments
+// needs more translation entries than the per-CU / per-XCD TLBs hold.
+__global__ void __launch_bounds__(256) block_random_kernel(const uint8_t* __restrict__ base, uint32_t kbs, int iters,
+                                                           u4v* __restrict__ sink, uint32_t zero) {
+    const uint32_t wave = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    u4v acc = {0, 0, 0, 0};
+    uint32_t h = wave * 2654435761u + 777u;
+    for (int i = 0; i < iters; i++) {
+        h ^= h << 13, h ^= h >> 17, h ^= h << 5;
+        const uint32_t kb = (h * 0x9e3779b1u >> 8) % kbs;
+        acc ^= *((const u4v*)(base + (uint64_t)kb * 1024) + lane);
+    }
+    if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == ~zero) sink[threadIdx.x] = acc;
+}
+
+hipError_t launch_block_random(const void* base, size_t bytes, int waves, int iters, void* sink, hipStream_t stream) {
+    hipLaunchKernelGGL(block_random_kernel, dim3(waves / 4), dim3(256), 0, stream, (const uint8_t*)base,
+                       (uint32_t)(bytes >> 10), iters, (u4v*)sink, 0u);
+    return hipGetLastError();
+}
+
+hipError_t launch_pool_scatter(const uint64_t* tab, int nslots, uint32_t fkb, uint32_t tkb, int lock, int waves,
+                               int iters, void* sink, hipStream_t stream) {
+    if (lock)
+        hipLaunchKernelGGL(pool_scatter_kernel<true>, dim3(waves / 4), dim3(256), 0, stream, tab, nslots, fkb, tkb,
+                           iters, (u4v*)sink, 0u);
+    else
+        hipLaunchKernelGGL(pool_scatter_kernel<false>, dim3(waves / 4), dim3(256), 0, stream, tab, nslots, fkb, tkb,
+                           iters, (u4v*)sink, 0u);
+    return hipGetLastError();
+}
+
+hipError_t launch_block_probe(void* p, size_t bytes, int rw, int reps, void* sink, hipStream_t stream) {
+    const size_t n = bytes / 16;
+    if (rw)
+        hipLaunchKernelGGL(block_probe_kernel<true>, dim3(2048), dim3(256), 0, stream, (u4v*)p, n, 0u, reps, (u4v*)sink);
+    else
+        hipLaunchKernelGGL(block_probe_kernel<false>, dim3(2048), dim3(256), 0, stream, (u4v*)p, n, 0u, reps, (u4v*)sink);
     return hipGetLastError();
 }
 

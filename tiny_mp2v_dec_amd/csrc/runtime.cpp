@@ -22,6 +22,10 @@ namespace mp2vg {
 hipError_t launch_recon(int cf, int mcm, const KArgs& a, hipStream_t stream);
 hipError_t launch_tile_convert(const KArgs& a, int cf, const int32_t* d_list, int n, int32_t slot0, hipStream_t stream);
 hipError_t launch_clock_probe(unsigned long long* d_out, int iters, int blocks, hipStream_t stream);
+hipError_t launch_block_probe(void* p, size_t bytes, int rw, int reps, void* sink, hipStream_t stream);
+hipError_t launch_block_random(const void* base, size_t bytes, int waves, int iters, void* sink, hipStream_t stream);
+hipError_t launch_pool_scatter(const uint64_t* tab, int nslots, uint32_t fkb, uint32_t tkb, int lock, int waves,
+                               int iters, void* sink, hipStream_t stream);
 hipError_t launch_digest(const uint64_t* ftab, const int32_t* d_slots, int n,
                          const uint64_t off[3], const int32_t stride[3], const int32_t w[3],
                          const int32_t h[3], unsigned long long* d_out, hipStream_t stream);
@@ -68,6 +72,7 @@ static const char* dev_env(const char* name) {
     return nullptr;
 #endif
 }
+static void pool_block_free(uint8_t* p, size_t bytes, uint64_t vmm);
 static size_t slot_pad() {
     const char* e = dev_env("MP2VG_SLOT_PAD");
     return e ? (size_t)std::max(0, atoi(e)) & ~(size_t)255 : 0;
@@ -143,6 +148,8 @@ struct mp2vg_ctx {
     // kernels index: [frames | tiles]); chunked pools (MP2VG_POOL_CHUNK slots per block) add blocks
     std::vector<uint64_t> fptr, tptr;
     std::vector<uint8_t*> chunks;
+    std::vector<size_t> chunk_bytes;  // allocation size of each block in `chunks`
+    std::vector<uint64_t> chunk_vmm;  // per block: its physical handle when mapped by pool_block_alloc (else 0)
     uint64_t* d_tab = nullptr;
     uint8_t* d_sink = nullptr;   // dummy loads / stores of the kernels (kPoolPad bytes)
     std::vector<uint8_t> tiles_ok;  // per slot: its tiles match its frame (after the batches enqueued)
@@ -224,6 +231,22 @@ extern "C" int mp2vg_create(const mp2vg_config_t* cfg, mp2vg_ctx_t** out) {
         return MP2VG_E_HIP;
     }
     HIPCHK(hipSetDevice(cfg->device));
+    // dev knob (placement study, profiles/r6/README.md): before the process's first context, N
+    // helper streams each submit one memset and are kept, so they take the first hardware queues
+    if (const char* qw = dev_env("MP2VG_QUEUE_WARM")) {
+        static bool warmed = false;
+        if (!warmed) {
+            warmed = true;
+            void* buf = nullptr;
+            if (hipMalloc(&buf, 4096) == hipSuccess)
+                for (int i = 0; i < atoi(qw); i++) {
+                    hipStream_t st;
+                    if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess)
+                        (void)hipMemsetAsync(buf, 0, 4096, st);
+                }
+            (void)hipDeviceSynchronize();
+        }
+    }
     mp2vg_ctx_t* c = new mp2vg_ctx_t();
     c->cfg = *cfg;
     c->g.init(cfg->width, cfg->height, cfg->chroma_format);
@@ -269,7 +292,7 @@ extern "C" int mp2vg_destroy(mp2vg_ctx_t* c) {
 
     hipFree(c->d_pool);
     hipFree(c->d_tiles);
-    for (auto q : c->chunks) hipFree(q);
+    for (size_t i = 0; i < c->chunks.size(); i++) pool_block_free(c->chunks[i], c->chunk_bytes[i], c->chunk_vmm[i]);
     hipFree(c->d_tab);
     hipFree(c->d_sink);
     for (Bank& b : c->bank) {
@@ -310,6 +333,66 @@ static int finish_reserve(mp2vg_ctx_t* c, int32_t nslots) {
     return MP2VG_OK;
 }
 
+// One pool block.  Default: hipMalloc.  Dev knobs for the placement study (profiles/r6/README.md):
+// MP2VG_POOL_POW2=1 rounds the block up to a power of two; MP2VG_POOL_VMM=<MB> maps it with the
+// virtual memory API at a VA aligned to that many MB (0 = the block's own power-of-two size).
+static hipError_t pool_block_alloc(int device, size_t bytes, uint8_t** p, size_t* got, uint64_t* vmm) {
+    *vmm = 0;
+    size_t sz = bytes;
+    const char* pw = dev_env("MP2VG_POOL_POW2");
+    const char* vm = dev_env("MP2VG_POOL_VMM");
+    if ((pw && atoi(pw)) || vm) {
+        sz = 1;
+        while (sz < bytes) sz <<= 1;
+    }
+    *got = sz;
+    if (!vm) return hipMalloc((void**)p, sz);
+    hipMemAllocationProp prop = {};
+    prop.type = hipMemAllocationTypePinned;
+    prop.location.type = hipMemLocationTypeDevice;
+    prop.location.id = device;
+    size_t gran = 0;
+    hipError_t e = hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityRecommended);
+    if (e != hipSuccess) return e;
+    sz = (sz + gran - 1) / gran * gran;
+    *got = sz;
+    const size_t align = atoi(vm) > 0 ? (size_t)atoi(vm) << 20 : sz;
+    hipMemGenericAllocationHandle_t h;
+    if ((e = hipMemCreate(&h, sz, &prop, 0)) != hipSuccess) return e;
+    void* va = nullptr;
+    if ((e = hipMemAddressReserve(&va, sz, align, nullptr, 0)) != hipSuccess) {
+        hipMemRelease(h);
+        return e;
+    }
+    if ((e = hipMemMap(va, sz, 0, h, 0)) != hipSuccess) {
+        hipMemAddressFree(va, sz);
+        hipMemRelease(h);
+        return e;
+    }
+    hipMemAccessDesc acc = {};
+    acc.location = prop.location;
+    acc.flags = hipMemAccessFlagsProtReadWrite;
+    if ((e = hipMemSetAccess(va, sz, &acc, 1)) != hipSuccess) {
+        hipMemUnmap(va, sz);
+        hipMemAddressFree(va, sz);
+        hipMemRelease(h);
+        return e;
+    }
+    *p = (uint8_t*)va;
+    *vmm = (uint64_t)(uintptr_t)h;
+    return hipSuccess;
+}
+
+static void pool_block_free(uint8_t* p, size_t bytes, uint64_t vmm) {
+    if (!vmm) {
+        hipFree(p);
+        return;
+    }
+    hipMemUnmap(p, bytes);
+    hipMemAddressFree(p, bytes);
+    hipMemRelease((hipMemGenericAllocationHandle_t)(uintptr_t)vmm);
+}
+
 extern "C" int mp2vg_reserve_slots(mp2vg_ctx_t* c, int32_t nslots) {
     if (!c || nslots <= 0) return MP2VG_E_INVALID;
     HIPCHK(hipSetDevice(c->cfg.device));
@@ -330,20 +413,27 @@ extern "C" int mp2vg_reserve_slots(mp2vg_ctx_t* c, int32_t nslots) {
         // the new blocks are committed to the context only once every allocation has succeeded: a
         // failed reserve leaves the pool (chunks, fptr, tptr, nslots) as it was, and frees its blocks
         std::vector<uint8_t*> blocks;
-        std::vector<uint64_t> fp, tp;
+        std::vector<size_t> bsz;
+        std::vector<uint64_t> fp, tp, vh;
         auto fail = [&](hipError_t e) {
-            for (uint8_t* q : blocks) hipFree(q);
+            for (size_t i = 0; i < blocks.size(); i++) pool_block_free(blocks[i], bsz[i], vh[i]);
             set_error(std::string("hipMalloc (frame pool block): ") + hipGetErrorString(e));
             return MP2VG_E_HIP;
         };
         for (int s0 = c->nslots; s0 < nslots; s0 += chunk) {
             const int k = std::min(chunk, nslots - s0);
             uint8_t *f = nullptr, *t = nullptr;
-            hipError_t e = hipMalloc((void**)&f, c->slot_stride * k + kPoolPad);
+            size_t got = 0;
+            uint64_t h = 0;
+            hipError_t e = pool_block_alloc(c->cfg.device, c->slot_stride * k + kPoolPad, &f, &got, &h);
             if (e != hipSuccess) return fail(e);
             blocks.push_back(f);
-            if ((e = hipMalloc((void**)&t, c->tile_stride * k)) != hipSuccess) return fail(e);
+            bsz.push_back(got);
+            vh.push_back(h);
+            if ((e = pool_block_alloc(c->cfg.device, c->tile_stride * k, &t, &got, &h)) != hipSuccess) return fail(e);
             blocks.push_back(t);
+            bsz.push_back(got);
+            vh.push_back(h);
             if ((e = hipMemsetAsync(f, 0, c->slot_stride * k + kPoolPad, c->stream)) != hipSuccess ||
                 (e = hipMemsetAsync(t, 0, c->tile_stride * k, c->stream)) != hipSuccess)
                 return fail(e);
@@ -353,6 +443,8 @@ extern "C" int mp2vg_reserve_slots(mp2vg_ctx_t* c, int32_t nslots) {
             }
         }
         c->chunks.insert(c->chunks.end(), blocks.begin(), blocks.end());
+        c->chunk_bytes.insert(c->chunk_bytes.end(), bsz.begin(), bsz.end());
+        c->chunk_vmm.insert(c->chunk_vmm.end(), vh.begin(), vh.end());
         c->fptr.insert(c->fptr.end(), fp.begin(), fp.end());
         c->tptr.insert(c->tptr.end(), tp.begin(), tp.end());
         return finish_reserve(c, nslots);
@@ -1144,6 +1236,62 @@ extern "C" int mp2vg_clock_probe(int32_t device, double* ghz) {
     hipFree(d);
     if (e != hipSuccess || h[1] == 0) return MP2VG_E_HIP;
     *ghz = (double)h[0] / (double)h[1] * 0.1;
+    return MP2VG_OK;
+}
+
+extern "C" int mp2vg_pool_probe(mp2vg_ctx_t* c, int32_t rw, int32_t reps, double* gbps, int32_t max,
+                                int32_t* nblocks) {
+    if (!c || !nblocks || max < 0 || (max > 0 && !gbps) || reps <= 0) return MP2VG_E_INVALID;
+    HIPCHK(hipSetDevice(c->cfg.device));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    for (hipStream_t s : c->sstreams) HIPCHK(hipStreamSynchronize(s));
+    hipEvent_t a, b;
+    HIPCHK(hipEventCreate(&a));
+    HIPCHK(hipEventCreate(&b));
+    hipError_t e = hipSuccess;
+    if (rw == 2 || rw == 3) {  // 2: random 1-KB reads over the pool, 3: many slots at one offset (one rate)
+        const int waves = 8192, iters = 256;
+        float ms = 0;
+        if (max > 0 && c->nslots > 0) {
+            e = hipEventRecord(a, c->stream);
+            for (int r = 0; r < reps && e == hipSuccess; r++)
+                e = launch_pool_scatter(c->d_tab, c->nslots, (uint32_t)(c->g.slot_bytes >> 10),
+                                        (uint32_t)((2 * c->g.slot_bytes) >> 10), rw == 3, waves, iters, c->d_sink,
+                                        c->stream);
+            if (e == hipSuccess) e = hipEventRecord(b, c->stream);
+            if (e == hipSuccess) e = hipEventSynchronize(b);
+            if (e == hipSuccess) e = hipEventElapsedTime(&ms, a, b);
+            gbps[0] = ms > 0 ? (double)waves * iters * 1024 * reps / (ms * 1e6) : 0.0;
+        }
+        hipEventDestroy(a);
+        hipEventDestroy(b);
+        if (e != hipSuccess) {
+            set_error(std::string("pool probe: ") + hipGetErrorString(e));
+            return MP2VG_E_HIP;
+        }
+        *nblocks = 1;
+        return MP2VG_OK;
+    }
+    const int n = std::min<int>(max, (int)c->chunks.size());
+    for (int i = 0; i < n && e == hipSuccess; i++) {
+        e = hipEventRecord(a, c->stream);
+        if (e == hipSuccess)
+            e = rw == 4 ? launch_block_random(c->chunks[i], c->chunk_bytes[i], 8192, 64 * reps, c->d_sink, c->stream)
+                        : launch_block_probe(c->chunks[i], c->chunk_bytes[i], rw, reps, c->d_sink, c->stream);
+        if (e == hipSuccess) e = hipEventRecord(b, c->stream);
+        if (e == hipSuccess) e = hipEventSynchronize(b);
+        float ms = 0;
+        if (e == hipSuccess) e = hipEventElapsedTime(&ms, a, b);
+        const double bytes = rw == 4 ? 8192.0 * 64 * reps * 1024 : (double)(c->chunk_bytes[i] & ~(size_t)15) * reps * (rw ? 2 : 1);
+        gbps[i] = ms > 0 ? bytes / (ms * 1e6) : 0.0;
+    }
+    hipEventDestroy(a);
+    hipEventDestroy(b);
+    if (e != hipSuccess) {
+        set_error(std::string("pool probe: ") + hipGetErrorString(e));
+        return MP2VG_E_HIP;
+    }
+    *nblocks = (int32_t)c->chunks.size();
     return MP2VG_OK;
 }
 

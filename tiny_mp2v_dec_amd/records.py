@@ -185,6 +185,19 @@ class DeviceContext:
         check(lib().mp2vg_batches_span(self.h, int(back_first), int(back_last), ctypes.byref(ms)), "batches_span")
         return ms.value
 
+    def pool_probe(self, rw=True, reps=4):
+        """Diagnostics: GB/s of each pool block (frames, tiles, frames, ... in allocation order)
+        under `reps` load(+store-back) sweeps; rw=2 / 3: one rate for random / same-offset 1-KB
+        reads over the pool; rw=4: per block, random 1-KB reads inside it; contents kept
+        (mp2vg_pool_probe)."""
+        n = ctypes.c_int32()
+        check(lib().mp2vg_pool_probe(self.h, int(rw), int(reps), None, 0, ctypes.byref(n)), "pool_probe")
+        n.value = 1 if int(rw) in (2, 3) else n.value
+        out = np.zeros(n.value, np.float64)
+        check(lib().mp2vg_pool_probe(self.h, int(rw), int(reps), out.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+                                     n.value, ctypes.byref(n)), "pool_probe")
+        return out
+
     def download(self, slot):
         """Visible planes of one slot: [Y, U, V] numpy arrays (height x width)."""
         planes = [np.empty((self.ph[i], self.pw[i]), np.uint8) for i in range(3)]

@@ -3,7 +3,7 @@
 # spread attribution), the drop-in frame modes, the intra dequant table on c1/c5/c2, and the I-only
 # configs at 4x their frame counts
 set -o pipefail
-AB='base head r2only base@MP2VG_STREAMS=1' ROUNDS=3 CFG=c2 bash tools/stamps_ab.sh r6g || exit 1
+AB='base head r2only base@MP2VG_STREAMS=1' ROUNDS=2 CFG=c2 bash tools/stamps_ab.sh r6g || exit 1
 cat gpurun_out/ab_r6g.txt
 bash tools/r6_dropin.sh || exit 1
 bash tools/r6_batch2.sh || exit 1
