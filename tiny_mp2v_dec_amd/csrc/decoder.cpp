@@ -349,10 +349,12 @@ extern "C" int mp2vg_decoder_decode(mp2vg_decoder_t* d, const uint8_t* buf, uint
     double t0 = now_ms(), tc;
     double t_up = 0, t_dec = 0, t_down = 0, t_wait = 0, t_gather = 0;
     ParseSession* ps = nullptr;
-    const int threads = d->cfg.num_threads > 0 ? d->cfg.num_threads : (int)std::thread::hardware_concurrency();
-    // (c2 stream, 768 frames, the GPU box's 16-CPU share, profiles/r5/dropin_threads.jsonl: 2 threads
-    // kept back 8.9-9.3k frames/s, 1 -> 9.7-9.9k, 0 -> 9.6-10.0k, 16 workers on 18 threads 9.4-9.6k)
-    int rc = parse_session_start(buf, len, &d->cfg, std::max(1, threads - 1), 4 * kChunk, &ps);
+    const int threads = d->cfg.num_threads > 0 ? d->cfg.num_threads : cpu_budget();
+    // Parse workers: the thread budget less three (this feed loop, its gather helpers, the render
+    // thread).  On the GPU box's 16-CPU quota (cgroup cpu.max on 256 CPUs) 15 workers of 16 threads
+    // left some decode() calls throttled (c2 3,072 frames, device frames: 5.9k next to 9.7-10.3k
+    // frames/s), 13 kept every call at 9.8-10.8k (profiles/r6/dropin_threads.jsonl).
+    int rc = parse_session_start(buf, len, &d->cfg, std::max(1, threads - 3), 4 * kChunk, &ps);
     t0 = trace_phase("dropin: headers", t0);
     if (rc != MP2VG_OK) return rc;
     std::unique_ptr<ParseSession, void (*)(ParseSession*)> guard(ps, parse_session_free);

@@ -865,7 +865,7 @@ int parse_session_start(const uint8_t* buf, uint64_t len, const mp2vg_config_t* 
         }
         if (held >= 0) res->display.push_back(held);
     }
-    int nthreads = threads > 0 ? threads : (int)std::thread::hardware_concurrency();
+    int nthreads = threads > 0 ? threads : cpu_budget();
     nthreads = std::max(1, std::min(nthreads, std::max(1, (int)S->jobs.size())));
     ParseSession* sp = S.get();
     for (int t = 0; t < nthreads; t++) sp->workers.emplace_back([sp]() { sp->work(); });
@@ -957,7 +957,7 @@ extern "C" int mp2vg_parse_es(const uint8_t* buf, uint64_t len, const mp2vg_conf
             }
         }
     };
-    int nthreads = cfg->num_threads > 0 ? cfg->num_threads : (int)std::thread::hardware_concurrency();
+    int nthreads = cfg->num_threads > 0 ? cfg->num_threads : cpu_budget();
     nthreads = std::max(1, std::min(nthreads, std::max(1, npics)));
     if (nthreads == 1) {
         copier();

@@ -327,6 +327,11 @@ void set_error(const std::string& msg);
 // returns when all calls have returned (tables.cpp)
 void parallel_for(int n, int max_threads, const std::function<void(int)>& fn);
 
+// CPUs this process may keep busy: the hardware threads, capped by the affinity mask and by a
+// cgroup v2 CPU quota (cpu.max "quota period": a container allowed 16 CPUs' time on a 256-CPU host
+// is throttled for the rest of each period once its threads have used it) (tables.cpp)
+int cpu_budget();
+
 // Host phase timing for diagnosis: with MP2VG_TRACE set, trace_phase(name, t0) prints the
 // milliseconds since t0 to stderr and returns the current time.
 double now_ms();

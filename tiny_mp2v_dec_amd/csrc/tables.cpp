@@ -1,3 +1,5 @@
+#include <sched.h>
+
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -192,10 +194,26 @@ class HelperPool {
 };
 }  // namespace
 
+int cpu_budget() {
+    static const int budget = [] {
+        int n = (int)std::thread::hardware_concurrency();
+        cpu_set_t set;
+        if (sched_getaffinity(0, sizeof(set), &set) == 0) n = std::min(n, std::max(1, CPU_COUNT(&set)));
+        if (FILE* f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
+            char q[32] = {0};
+            long long period = 0;
+            if (fscanf(f, "%31s %lld", q, &period) == 2 && period > 0 && q[0] >= '0' && q[0] <= '9')
+                n = std::min(n, (int)std::max(1LL, atoll(q) / period));
+            fclose(f);
+        }
+        return std::max(1, n);
+    }();
+    return budget;
+}
+
 void parallel_for(int n, int max_threads, const std::function<void(int)>& fn) {
     if (n <= 0) return;
-    static HelperPool* pool = new HelperPool(
-        std::max(0, std::min(15, (int)std::thread::hardware_concurrency() - 1)));  // never destroyed
+    static HelperPool* pool = new HelperPool(std::max(0, std::min(15, cpu_budget() - 1)));  // never destroyed
     const int helpers = std::min({max_threads - 1, pool->size(), n - 1});
     if (helpers <= 0) {
         for (int i = 0; i < n; i++) fn(i);

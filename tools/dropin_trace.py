@@ -4,7 +4,7 @@ with `both` also device frames, MP2VG_DECODER_DEVICE_FRAMES; 16 threads), runs o
 interleaved; prints frames/s per run, and MP2VG_TRACE's per-phase lines go to stderr, for telling
 a slow run's phase.
 
-    MP2VG_TRACE=1 python tools/dropin_trace.py [gops] [host|device|both] [runs] 2> trace.txt
+    MP2VG_TRACE=1 python tools/dropin_trace.py [gops] [host|device|both] [runs] [threads] 2> trace.txt
 """
 import json
 import os
@@ -19,10 +19,11 @@ from tiny_mp2v_dec_amd.decoder import decoder_config_t, mp2v_decoder_c  # noqa: 
 gops = int(sys.argv[1]) if len(sys.argv) > 1 else 64
 modes = {"host": [False], "device": [True], "both": [False, True]}[sys.argv[2] if len(sys.argv) > 2 else "host"]
 runs = int(sys.argv[3]) if len(sys.argv) > 3 else 6
+threads = int(sys.argv[4]) if len(sys.argv) > 4 else 16
 w, h, cf, extra, _ = bench.CONFIGS["c2"]
 es = R.generate_es(width=w, height=h, chroma_format=cf, n_gops=gops, seed=1729, **extra)
 n = [0]
-decs = {m: mp2v_decoder_c(decoder_config_t(w, h, cf, pictures_pool_size=24, num_threads=16, device_frames=m),
+decs = {m: mp2v_decoder_c(decoder_config_t(w, h, cf, pictures_pool_size=24, num_threads=threads, device_frames=m),
                           lambda f: n.__setitem__(0, n[0] + 1)) for m in modes}
 for run in range(runs):
     for m in modes:
@@ -31,6 +32,6 @@ for run in range(runs):
         t0 = time.perf_counter()
         decs[m].decode(es)
         dt = time.perf_counter() - t0
-        print(json.dumps({"run": run, "device_frames": m, "frames": n[0], "frames_per_s": round(n[0] / dt, 1)}), flush=True)
+        print(json.dumps({"run": run, "threads": threads, "device_frames": m, "frames": n[0], "frames_per_s": round(n[0] / dt, 1)}), flush=True)
 for d in decs.values():
     d.close()
