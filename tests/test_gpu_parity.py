@@ -213,19 +213,18 @@ def test_one_direction_b_pictures_through_the_p_loop(cf):
 
 
 @pytest.mark.parametrize("cf", [1, 2, 3])
-def test_tile_free_i_launch_then_predictions(cf):
-    """A 4:2:0 / 4:2:2 I-only batch in which few pictures store anchor tiles runs the I kernel
-    without its tile store code (launch mode 4) and converts the tiles of the pictures a later
-    batch may read (the last two) right after the launch (runtime.cpp plan_batch / TilePlan); the
-    4:4:4 batch keeps the tile-storing kernel.  Batch 1: 12 I pictures; batch 2: a P picture
-    predicting from picture 11 and B pictures from pictures 11 and 10, read through the tiles;
-    every frame vs the oracle."""
+def test_i_only_batch_then_predictions(cf):
+    """An I-only batch in which few pictures store anchor tiles (the last two, which a later batch
+    may read; runtime.cpp plan_batch / TilePlan) stores exactly those pictures' tiles from the I
+    kernel (mode 0; the tile-free mode 4 is a dev switch).  Batch 1: 12 I pictures; batch 2: a P
+    picture predicting from picture 11 and B pictures from pictures 11 and 10, read through the
+    tiles; every frame vs the oracle."""
     w, h = 96, 64
     pics, mbs, coefs = random_batch(w, h, cf, 16, seed=5150 + cf, n_intra=12)
     exp = oracle_frames(_P(w, h, cf, pics, mbs, coefs))
     n = (w // 16) * (h // 16)
     c0 = int(mbs["coef_off"][12 * n])
-    assert set(R.plan_batch(w, h, cf, 16, pics[:12], mbs[:12 * n], coefs[:c0])[1].tolist()) == {4 if cf < 3 else 0}
+    assert set(R.plan_batch(w, h, cf, 16, pics[:12], mbs[:12 * n], coefs[:c0])[1].tolist()) == {0}
     p2 = pics[12:].copy()
     p2["mb_first"] -= 12 * n
     m2 = mbs[12 * n:].copy()

@@ -163,17 +163,14 @@ def test_parser_output_of_mutated_streams_passes_full_validation(cf, seed):
 
 
 def test_i_only_launch_modes():
-    """I-only launches in which at most a quarter of the pictures store anchor tiles (an I-only
-    stream: only the batch's last two, which the next batch may read) run the tile-free I kernel,
-    mode 4 (runtime.cpp plan_batch); every I launch of an IPB stream stores tiles (mode 0)."""
+    """Every I-only launch of a product library runs the tile-storing I kernel (mode 0); the
+    tile-free I kernel (mode 4, runtime.cpp plan_batch) is a dev-build switch (MP2VG_I_TILEFREE),
+    measured neutral on c1 in two rounds."""
     w, h = 176, 144
     es = R.generate_es(width=w, height=h, chroma_format=1, n_gops=16, gop_n=1, gop_m=1, seed=3)
     p = R.Parsed(es, w, h, 1)
-    assert R.plan_batch(w, h, 1, p.npics, p.pics, p.mbs, p.coefs)[1].tolist() == [4, 4]
-    assert R.plan_batch(w, h, 1, p.npics, p.pics, p.mbs, p.coefs, one_stream=True)[1].tolist() == [4]
-    # four pictures, two per set: one of each set's two stores tiles -> the tile-storing kernel
-    q = R.Parsed(R.generate_es(width=w, height=h, chroma_format=1, n_gops=4, gop_n=1, gop_m=1, seed=3), w, h, 1)
-    assert R.plan_batch(w, h, 1, q.npics, q.pics, q.mbs, q.coefs)[1].tolist() == [0, 0]
+    assert R.plan_batch(w, h, 1, p.npics, p.pics, p.mbs, p.coefs)[1].tolist() == [0, 0]
+    assert R.plan_batch(w, h, 1, p.npics, p.pics, p.mbs, p.coefs, one_stream=True)[1].tolist() == [0]
     g = _parsed(1)
     modes = R.plan_batch(g.width, g.height, 1, g.npics, g.pics, g.mbs, g.coefs)[1].tolist()
     assert 0 in modes and 4 not in modes

@@ -817,15 +817,15 @@ static int plan_batch(mp2vg_ctx_t* c, const mp2vg_picture_t* pics, int32_t npics
         }
         l.end = (uint32_t)slices.size();
         l.mcm = types == 1 ? 0 : (types == 2 ? 1 : (types == 4 ? 2 : 3));
-        // A 4:2:0 / 4:2:2 I-only launch in which at most a quarter of the pictures store tiles (an
+        // (dev) A 4:2:0 / 4:2:2 I-only launch in which at most a quarter of the pictures store tiles (an
         // I-only stream: the batch's last two pictures) runs the I kernel without the tile store
         // code (mode 4: 71 instead of 79 VGPRs, 7 waves per SIMD instead of 6; the 4:4:4 kernel
         // keeps its 4) and converts those pictures' tiles after it (tile_convert, same stream).
-        // Measured neutral on c1 (one-stream I launch 0.286 ms either way, profiles/r5/README.md):
-        // the skipped stores were already branched over per slice.  (MP2VG_I_TILEFREE=0 in dev
-        // builds keeps mode 0.)
-        // (MP2VG_I_TILEFREE=2 in dev builds: every I-only launch, whatever stores tiles, 4:4:4 too)
-        static const int tilefree = !dev_env("MP2VG_I_TILEFREE") ? 1 : atoi(dev_env("MP2VG_I_TILEFREE"));
+        // Measured neutral on c1 twice (one-stream I launch 0.286 ms either way, profiles/r5/README.md;
+        // 388-419k against 402-419k frames/s, profiles/r6/ab_mode4_c1.txt): the skipped stores were
+        // already branched over per slice.  So a dev switch only: MP2VG_I_TILEFREE=1 in dev builds
+        // enables it, =2 runs it for every I-only launch, whatever stores tiles, 4:4:4 too.
+        static const int tilefree = dev_env("MP2VG_I_TILEFREE") ? atoi(dev_env("MP2VG_I_TILEFREE")) : 0;
         int nneed = 0;
         for (int p : lp) nneed += need[p];
         if (types == 1 && (tilefree == 2 || (tilefree && c->g.cf != 3 && nneed * 4 <= (int)lp.size()))) {
