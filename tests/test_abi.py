@@ -69,6 +69,10 @@ def test_invalid_arguments_rejected():
     assert L.mp2vg_create(None, None) == -1
     assert L.mp2vg_batch_decode(None) == -1
     assert L.mp2vg_destroy(None) == -1
+    n = ctypes.c_int32()
+    assert L.mp2vg_pool_probe(None, 1, 1, None, 0, ctypes.byref(n)) == -1
+    assert L.mp2vg_clock_probe(0, None) == -1
+    assert L.mp2vg_sink_device_ptr(None, None) == -1
 
 
 def test_no_silent_cpu_fallback_without_gpu():

@@ -466,3 +466,29 @@ def test_product_library_refuses_dev_ablations():
     env = dict(os.environ, MP2VG_ABLATE="1")
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and "refused" in r.stdout, (r.returncode, r.stdout[-500:], r.stderr[-1500:])
+
+
+def test_pool_probes_keep_the_decoded_frames():
+    """The placement diagnostics (mp2vg_pool_probe: load and load+store-back sweeps per pool
+    block, random and same-offset 1-KB reads over the pool, random reads inside each block) and
+    the clock probe leave every decoded slot as it was, and report positive rates."""
+    import ctypes
+    from tiny_mp2v_dec_amd._lib import lib
+    es = R.generate_es(width=176, height=144, chroma_format=1, n_gops=2, gop_n=6, gop_m=3, seed=77)
+    parsed = R.Parsed(es, 176, 144, 1)
+    with R.DeviceContext(176, 144, 1, slots=parsed.npics) as ctx:
+        ctx.upload(parsed.pics, parsed.mbs, parsed.coefs)
+        ctx.decode()
+        ctx.synchronize()
+        before = ctx.digests(np.arange(parsed.npics))
+        for mode in range(5):
+            rates = ctx.pool_probe(rw=mode, reps=1)
+            assert len(rates) >= 1 and (rates > 0).all(), (mode, rates)
+        assert np.array_equal(ctx.digests(np.arange(parsed.npics)), before)
+        exp = oracle_frames(parsed)
+        for p in range(parsed.npics):
+            got = ctx.download(p)
+            for k in range(3):
+                assert np.array_equal(got[k], exp[p][k]), (p, k)
+    ghz = ctypes.c_double()
+    assert lib().mp2vg_clock_probe(0, ctypes.byref(ghz)) == 0 and 0.5 < ghz.value < 4.0
