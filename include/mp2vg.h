@@ -214,7 +214,9 @@ int  mp2vg_clock_probe(int32_t device, double* ghz);
  * that load every 16-B word and, with rw = 1, store it back unchanged.  gbps[i] for the first
  * `max` blocks; *nblocks = the pool's block count.  rw = 2: one rate (gbps[0], *nblocks = 1) for
  * 1-KB reads at random slots and offsets over the whole pool; rw = 3: the same with many slots read
- * at one offset at a time; rw = 4: per block, random 1-KB reads inside the block.  Synchronises
+ * at one offset at a time; rw = 4: per block, random 1-KB reads inside the block; rw = 5: load
+ * sweeps over the two record banks (MB records, coefficient words: 4 rates, 0 where a bank is
+ * not allocated); rw = 6 / 7: rw = 3 / 2 with each 1-KB run stored back unchanged.  Synchronises
  * the context; contents kept. */
 int  mp2vg_pool_probe(mp2vg_ctx_t* ctx, int32_t rw, int32_t reps, double* gbps, int32_t max, int32_t* nblocks);
 /* 64-bit order-independent digest of each listed slot's visible planes, computed on device:

@@ -481,9 +481,10 @@ def test_pool_probes_keep_the_decoded_frames():
         ctx.decode()
         ctx.synchronize()
         before = ctx.digests(np.arange(parsed.npics))
-        for mode in range(5):
+        for mode in range(8):
             rates = ctx.pool_probe(rw=mode, reps=1)
-            assert len(rates) >= 1 and (rates > 0).all(), (mode, rates)
+            # (mode 5: the second record bank is allocated only once a second batch is uploaded)
+            assert len(rates) >= 1 and ((rates > 0).any() if mode == 5 else (rates > 0).all()), (mode, rates)
         assert np.array_equal(ctx.digests(np.arange(parsed.npics)), before)
         exp = oracle_frames(parsed)
         for p in range(parsed.npics):

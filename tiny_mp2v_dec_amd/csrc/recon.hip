@@ -1774,7 +1774,7 @@ __global__ void __launch_bounds__(256) block_probe_kernel(u4v* __restrict__ p, s
 // LOCK = false: each run in a random slot (frame or tile), at a random 1-KB offset (a page-walk /
 // TLB-reach probe); true: wave w reads slot w % nslots, and run i of every wave sits at the same
 // offset i * 4 KB in its slot (many pictures at one offset at once: the decode's access shape).
-template <bool LOCK>
+template <bool LOCK, bool RW = false>
 __global__ void __launch_bounds__(256) pool_scatter_kernel(const uint64_t* __restrict__ tab, int nslots,
                                                            uint32_t fkb, uint32_t tkb, int iters,
                                                            u4v* __restrict__ sink, uint32_t zero) {
@@ -1794,8 +1794,14 @@ __global__ void __launch_bounds__(256) pool_scatter_kernel(const uint64_t* __res
             const uint32_t g = h * 0x9e3779b1u;
             kb = (g >> 8) % (tile ? tkb : fkb);
         }
-        const u4v* p = (const u4v*)(tab[tile * nslots + slot] + (uint64_t)kb * 1024) + lane;
-        acc ^= *p;
+        u4v* p = (u4v*)(tab[tile * nslots + slot] + (uint64_t)kb * 1024) + lane;
+        u4v v = *p;
+        if (RW) {  // stored back unchanged (xor a runtime 0)
+            v.x ^= zero;
+            *p = v;
+        } else {
+            acc ^= v;
+        }
     }
     if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == ~zero) sink[threadIdx.x] = acc;
 }
@@ -1823,7 +1829,10 @@ hipError_t launch_block_random(const void* base, size_t bytes, int waves, int it
 
 hipError_t launch_pool_scatter(const uint64_t* tab, int nslots, uint32_t fkb, uint32_t tkb, int lock, int waves,
                                int iters, void* sink, hipStream_t stream) {
-    if (lock)
+    if (lock >= 2)  // 2: same offsets, loaded and stored back; 3: random, loaded and stored back
+        hipLaunchKernelGGL((lock == 2 ? pool_scatter_kernel<true, true> : pool_scatter_kernel<false, true>),
+                           dim3(waves / 4), dim3(256), 0, stream, tab, nslots, fkb, tkb, iters, (u4v*)sink, 0u);
+    else if (lock)
         hipLaunchKernelGGL(pool_scatter_kernel<true>, dim3(waves / 4), dim3(256), 0, stream, tab, nslots, fkb, tkb,
                            iters, (u4v*)sink, 0u);
     else

@@ -1249,19 +1249,49 @@ extern "C" int mp2vg_pool_probe(mp2vg_ctx_t* c, int32_t rw, int32_t reps, double
     HIPCHK(hipEventCreate(&a));
     HIPCHK(hipEventCreate(&b));
     hipError_t e = hipSuccess;
-    if (rw == 2 || rw == 3) {  // 2: random 1-KB reads over the pool, 3: many slots at one offset (one rate)
+    if (rw == 5) {  // the record banks: a load sweep over each bank's MB records and coefficient words
+        int n = 0;
+        for (Bank& bk : c->bank) {
+            const std::pair<void*, size_t> bufs[2] = {{bk.d_mbs, bk.cap_mbs * sizeof(mp2vg_mb_t)},
+                                                      {bk.d_coefs, bk.cap_coefs * sizeof(uint32_t)}};
+            for (const auto& q : bufs) {
+                if (n >= max) break;
+                float ms = 0;
+                if (q.first && q.second >= 16) {
+                    e = hipEventRecord(a, c->stream);
+                    if (e == hipSuccess) e = launch_block_probe(q.first, q.second & ~(size_t)15, 0, reps, c->d_sink, c->stream);
+                    if (e == hipSuccess) e = hipEventRecord(b, c->stream);
+                    if (e == hipSuccess) e = hipEventSynchronize(b);
+                    if (e == hipSuccess) e = hipEventElapsedTime(&ms, a, b);
+                }
+                gbps[n++] = ms > 0 ? (double)(q.second & ~(size_t)15) * reps / (ms * 1e6) : 0.0;
+                if (e != hipSuccess) break;
+            }
+        }
+        hipEventDestroy(a);
+        hipEventDestroy(b);
+        if (e != hipSuccess) {
+            set_error(std::string("pool probe: ") + hipGetErrorString(e));
+            return MP2VG_E_HIP;
+        }
+        *nblocks = 4;
+        return MP2VG_OK;
+    }
+    if (rw == 2 || rw == 3 || rw == 6 || rw == 7) {  // 2: random 1-KB reads over the pool, 3: many slots at one
+                                                      // offset (one rate); 6 / 7: 3 / 2 with each run stored back
         const int waves = 8192, iters = 256;
         float ms = 0;
         if (max > 0 && c->nslots > 0) {
             e = hipEventRecord(a, c->stream);
             for (int r = 0; r < reps && e == hipSuccess; r++)
                 e = launch_pool_scatter(c->d_tab, c->nslots, (uint32_t)(c->g.slot_bytes >> 10),
-                                        (uint32_t)((2 * c->g.slot_bytes) >> 10), rw == 3, waves, iters, c->d_sink,
+                                        (uint32_t)((2 * c->g.slot_bytes) >> 10),
+                                        rw == 3 ? 1 : rw == 6 ? 2 : rw == 7 ? 3 : 0, waves, iters, c->d_sink,
                                         c->stream);
             if (e == hipSuccess) e = hipEventRecord(b, c->stream);
             if (e == hipSuccess) e = hipEventSynchronize(b);
             if (e == hipSuccess) e = hipEventElapsedTime(&ms, a, b);
-            gbps[0] = ms > 0 ? (double)waves * iters * 1024 * reps / (ms * 1e6) : 0.0;
+            gbps[0] = ms > 0 ? (double)waves * iters * 1024 * reps * (rw >= 6 ? 2 : 1) / (ms * 1e6) : 0.0;
         }
         hipEventDestroy(a);
         hipEventDestroy(b);

@@ -188,11 +188,12 @@ class DeviceContext:
     def pool_probe(self, rw=True, reps=4):
         """Diagnostics: GB/s of each pool block (frames, tiles, frames, ... in allocation order)
         under `reps` load(+store-back) sweeps; rw=2 / 3: one rate for random / same-offset 1-KB
-        reads over the pool; rw=4: per block, random 1-KB reads inside it; contents kept
+        reads over the pool; rw=4: per block, random 1-KB reads inside it; rw=5: the two record
+        banks' MB records and coefficient words; contents kept
         (mp2vg_pool_probe)."""
         n = ctypes.c_int32()
         check(lib().mp2vg_pool_probe(self.h, int(rw), int(reps), None, 0, ctypes.byref(n)), "pool_probe")
-        n.value = 1 if int(rw) in (2, 3) else n.value
+        n.value = 1 if int(rw) in (2, 3, 6, 7) else (4 if int(rw) == 5 else n.value)
         out = np.zeros(n.value, np.float64)
         check(lib().mp2vg_pool_probe(self.h, int(rw), int(reps), out.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
                                      n.value, ctypes.byref(n)), "pool_probe")

@@ -102,6 +102,13 @@ def main():
         ref = d
     # per-block HBM rate of each context's pool (frames and tiles blocks alternate)
     probe = {}
+    for i, c in enumerate(ctxs):  # the record banks (cheap: one sweep each)
+        rnd = [round(float(c.pool_probe(rw=2, reps=4)[0])) for _ in range(2)]
+        lck = [round(float(c.pool_probe(rw=3, reps=4)[0])) for _ in range(2)]
+        rndw = [round(float(c.pool_probe(rw=7, reps=4)[0])) for _ in range(2)]
+        lckw = [round(float(c.pool_probe(rw=6, reps=4)[0])) for _ in range(2)]
+        print(f"ctx {i} GB/s 1-KB runs: random {rnd} same-offset {lck} | stored back: random {rndw} "
+              f"same-offset {lckw}", flush=True)
     for i, c in enumerate([] if a.no_probe else ctxs):
         rw = c.pool_probe(rw=1, reps=4)
         ro = c.pool_probe(rw=0, reps=4)
