@@ -339,6 +339,12 @@ def main():
     alg_bytes, parts = algorithmic_bytes(parsed)
     ctx = R.DeviceContext(width, height, cf, slots=parsed.npics, device=device)
     ctx.upload(parsed.pics, parsed.mbs, parsed.coefs)
+    # the one-stream context of the per-kernel lines (used after the timed region); with
+    # MP2VG_BENCH_CTX1_EARLY=1 (measurements) it takes its pool now, before ctx's first batch
+    ctx1 = None
+    if os.environ.get("MP2VG_BENCH_CTX1_EARLY") == "1":
+        ctx1 = R.DeviceContext(width, height, cf, slots=parsed.npics, device=device, one_stream=True)
+        ctx1.upload(parsed.pics, parsed.mbs, parsed.coefs)
 
     for _ in range(args.warmup):
         ctx.decode()
@@ -367,6 +373,8 @@ def main():
     # device span of the timed steps: first batch start -> last batch end (consecutive batches
     # overlap picture set by picture set, runtime.cpp mp2vg_batch_decode)
     device_span_ms = ctx.batches_span(timed - 1, 0)
+    # the runtime's pool placement calibration at the context's first (warm-up) batch
+    place_ms, place_kept = ctx.placement()
     elapsed = G.max_over_ranks(elapsed, dist, coll_dev)
 
     # ---- parity of the timed batch: device digest of every frame vs the compiled reference's ----
@@ -379,8 +387,9 @@ def main():
                                  one_stream=True)
     pic_bytes = per_picture_bytes(parsed)
     launch_bytes = np.bincount(of_pic, weights=pic_bytes, minlength=len(modes))
-    ctx1 = R.DeviceContext(width, height, cf, slots=parsed.npics, device=device, one_stream=True)
-    ctx1.upload(parsed.pics, parsed.mbs, parsed.coefs)
+    if ctx1 is None:
+        ctx1 = R.DeviceContext(width, height, cf, slots=parsed.npics, device=device, one_stream=True)
+        ctx1.upload(parsed.pics, parsed.mbs, parsed.coefs)
     k1 = 5
     for _ in range(k1 + 1):
         ctx1.decode()
@@ -468,6 +477,10 @@ def main():
                      "dominant_kernel": dominant, "one_stream_span_ms": round(span1, 4),
                      "per_kernel": per_kernel},
         "box": {"shader_clock_ghz_valu_load": clock_ghz, "host_cpus_visible": os.cpu_count()},
+        "pool_placement": {"candidate_batch_ms": place_ms, "kept": place_kept,
+                           "note": "runtime.cpp calibrate_placement, at the first warm-up batch: the batch "
+                                   "decoded on the pool and on copies in fresh blocks (round 0 of each, then "
+                                   "round 1), the fastest pool kept; outside the timed region"},
         "frame_digest_of_digests": int(np.bitwise_xor.reduce(np.concatenate(gathered))),
         "provenance": _build.provenance(),
     }

@@ -493,3 +493,36 @@ def test_pool_probes_keep_the_decoded_frames():
                 assert np.array_equal(got[k], exp[p][k]), (p, k)
     ghz = ctypes.c_double()
     assert lib().mp2vg_clock_probe(0, ctypes.byref(ghz)) == 0 and 0.5 < ghz.value < 4.0
+
+
+def test_pool_placement_calibration_keeps_every_frame(monkeypatch):
+    """The runtime's placement calibration (calibrate_placement: at a large pool's first batch the
+    batch is decoded on the pool and on copies of it in fresh blocks, and the fastest pool is
+    kept), forced on a small pool: batch 1 (12 I pictures) is calibrated over 3 pools, batch 2 (P
+    and B pictures predicting from batch 1's slots 10 and 11) reads the kept pool; every frame of
+    both vs the oracle, and the calibration ran (2 rounds x 3 candidate times)."""
+    monkeypatch.setenv("MP2VG_PLACE_CANDIDATES", "3")
+    monkeypatch.setenv("MP2VG_PLACE_MIN_MB", "0")
+    w, h, cf = 96, 64, 1
+    pics, mbs, coefs = random_batch(w, h, cf, 16, seed=8080, n_intra=12)
+    exp = oracle_frames(_P(w, h, cf, pics, mbs, coefs))
+    n = (w // 16) * (h // 16)
+    c0 = int(mbs["coef_off"][12 * n])
+    p2 = pics[12:].copy()
+    p2["mb_first"] -= 12 * n
+    m2 = mbs[12 * n:].copy()
+    m2["coef_off"] -= c0
+    with R.DeviceContext(w, h, cf, slots=16) as ctx:
+        ctx.upload(pics[:12], mbs[:12 * n], coefs[:c0])
+        ctx.decode()
+        ctx.synchronize()
+        ms, kept = ctx.placement()
+        assert len(ms) == 6 and 0 <= kept < 3 and all(t > 0 for t in ms)
+        ctx.upload(p2, m2, coefs[c0:])
+        ctx.decode()
+        ctx.synchronize()
+        assert ctx.placement() == (ms, kept)  # once per context
+        for p in range(16):
+            got = ctx.download(p)
+            for k in range(3):
+                assert np.array_equal(got[k], exp[p][k]), (p, k)

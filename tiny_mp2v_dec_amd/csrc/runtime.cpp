@@ -175,6 +175,9 @@ struct mp2vg_ctx {
     uint64_t seq = 0;  // batches decoded
     hipEvent_t up_ev[2] = {nullptr, nullptr};  // staging halves of upload()
     bool launch_timing = true;  // per-launch events (mp2vg_last_launch_times)
+    bool placed = false;        // the pool's placement was calibrated (calibrate_placement)
+    std::vector<float> place_ms;  // its batch times: round 0 of every candidate, then round 1
+    int place_kept = -1;          // the candidate kept (0 = the pool as first allocated)
 
     void* h_stage = nullptr;
     int32_t* d_dslots = nullptr;
@@ -975,6 +978,167 @@ hipStream_t ctx_stream(mp2vg_ctx_t* c) { return c->stream; }
 void ctx_set_launch_timing(mp2vg_ctx_t* c, bool on) { c->launch_timing = on; }
 }  // namespace mp2vg
 
+static int batch_decode(mp2vg_ctx_t* c);
+
+// ---- pool placement calibration ------------------------------------------------------------
+// Identical contexts in one process decode the same batch up to 13 % apart, each keeping its
+// speed, and which one is slow is not predicted by any per-block or pool-wide bandwidth probe
+// (profiles/r6/README.md §8).  So a large pool measures its own placement once: at its first
+// batch, the pool is copied into MP2VG_PLACE_CANDIDATES - 1 freshly allocated pools (same block
+// sizes), the batch is decoded on each from the same starting state, and the pool with the
+// shortest batch is kept (the others are freed).  Every candidate ends in the same state (the
+// batch decoded), so the choice changes no output.
+struct PoolSet {
+    std::vector<uint8_t*> chunks;
+    std::vector<size_t> bytes;
+    std::vector<uint64_t> vmm, fptr, tptr;
+};
+
+static void pool_set_free(PoolSet& p) {
+    for (size_t i = 0; i < p.chunks.size(); i++) pool_block_free(p.chunks[i], p.bytes[i], p.vmm[i]);
+    p = PoolSet();
+}
+
+static PoolSet pool_take(mp2vg_ctx_t* c) {
+    PoolSet p;
+    p.chunks.swap(c->chunks);
+    p.bytes.swap(c->chunk_bytes);
+    p.vmm.swap(c->chunk_vmm);
+    p.fptr.swap(c->fptr);
+    p.tptr.swap(c->tptr);
+    return p;
+}
+
+static hipError_t pool_install(mp2vg_ctx_t* c, PoolSet& p) {
+    c->chunks.swap(p.chunks);
+    c->chunk_bytes.swap(p.bytes);
+    c->chunk_vmm.swap(p.vmm);
+    c->fptr.swap(p.fptr);
+    c->tptr.swap(p.tptr);
+    p = PoolSet();
+    hipError_t e = hipMemcpyAsync(c->d_tab, c->fptr.data(), sizeof(uint64_t) * c->nslots, hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(c->d_tab + c->nslots, c->tptr.data(), sizeof(uint64_t) * c->nslots, hipMemcpyHostToDevice,
+                           c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    return e;
+}
+
+// a copy of pool `src` (blocks of the same sizes, contents copied, slot addresses rebased)
+static hipError_t pool_clone(mp2vg_ctx_t* c, const PoolSet& src, PoolSet& dst) {
+    for (size_t i = 0; i < src.chunks.size(); i++) {
+        uint8_t* q = nullptr;
+        size_t got = 0;
+        uint64_t h = 0;
+        hipError_t e = pool_block_alloc(c->cfg.device, src.bytes[i], &q, &got, &h);
+        if (e != hipSuccess) {
+            pool_set_free(dst);
+            return e;
+        }
+        dst.chunks.push_back(q);
+        dst.bytes.push_back(got);
+        dst.vmm.push_back(h);
+        if ((e = hipMemcpyAsync(q, src.chunks[i], src.bytes[i], hipMemcpyDeviceToDevice, c->stream)) != hipSuccess) {
+            pool_set_free(dst);
+            return e;
+        }
+    }
+    // blocks sorted by address, to map each slot pointer to its block
+    std::vector<std::pair<uintptr_t, size_t>> order(src.chunks.size());
+    for (size_t i = 0; i < order.size(); i++) order[i] = {(uintptr_t)src.chunks[i], i};
+    std::sort(order.begin(), order.end());
+    auto rebase = [&](uint64_t ptr) -> uint64_t {
+        auto it = std::upper_bound(order.begin(), order.end(), std::make_pair((uintptr_t)ptr, (size_t)-1));
+        const size_t i = std::prev(it)->second;
+        return (uint64_t)(uintptr_t)dst.chunks[i] + (ptr - (uint64_t)(uintptr_t)src.chunks[i]);
+    };
+    for (uint64_t f : src.fptr) dst.fptr.push_back(rebase(f));
+    for (uint64_t t : src.tptr) dst.tptr.push_back(rebase(t));
+    return hipStreamSynchronize(c->stream);
+}
+
+// MP2VG_PLACE_CANDIDATES (pools tried, 1 = off; default 3), MP2VG_PLACE_MIN_MB (smallest pool
+// calibrated; default 4096), MP2VG_PLACE_ONE_STREAM=1 (one-stream contexts too)
+static int env_int(const char* name, int dflt) {
+    const char* e = getenv(name);
+    return e && *e ? atoi(e) : dflt;
+}
+
+// returns 1 when it did not run (the caller decodes), else the status of the calibrated decode.
+// The batch is decoded 2 + 2 x candidates times: twice on the first pool (the GPU's clocks ramp
+// over the first tens of ms of work: first-round times fall pool after pool whatever the pool),
+// then twice on every candidate, round-robin, each candidate's time its faster run.  Decoding a
+// batch again from its own output is exact only when no slot it writes is one it reads from
+// before the batch (TilePlan.ext_reads); other batches are decoded once, uncalibrated.
+static int calibrate_placement(mp2vg_ctx_t* c) {
+    if (c->placed) return 1;
+    const int k = std::max(1, std::min(4, env_int("MP2VG_PLACE_CANDIDATES", 3)));
+    size_t pool = 0;
+    for (size_t b : c->chunk_bytes) pool += b;
+    if (k < 2 || c->chunks.empty() || pool < ((size_t)std::max(0, env_int("MP2VG_PLACE_MIN_MB", 4096)) << 20)) return 1;
+    // (a one-stream context is the bench's per-kernel measurement context: calibrated, it ran its
+    // later batches 5 % slower than its calibration runs, a cause not found; off unless asked)
+    if (c->nstreams == 1 && !env_int("MP2VG_PLACE_ONE_STREAM", 0)) return 1;
+    const Bank& bk = c->bank[c->cur];
+    std::vector<uint8_t> written(c->nslots, 0);
+    for (const auto& w : bk.tiles.writes)
+        if (w.first >= 0 && w.first < c->nslots) written[w.first] = 1;
+    for (const auto& r : bk.tiles.ext_reads)
+        if (r.first >= 0 && r.first < c->nslots && written[r.first]) return 1;
+    c->placed = true;
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) return 1;
+    HIPCHK(hipStreamSynchronize(c->stream));
+    std::vector<PoolSet> cand;
+    cand.push_back(pool_take(c));
+    // (candidates only while the device keeps 8 GB free beside them)
+    for (int i = 1; i < k && free_b > (size_t)i * pool + ((size_t)8 << 30); i++) {
+        PoolSet p;
+        if (pool_clone(c, cand[0], p) != hipSuccess) {
+            (void)hipGetLastError();
+            break;
+        }
+        cand.push_back(std::move(p));
+    }
+    const size_t n = cand.size();
+    std::vector<float> ms(2 * n, 0.f);
+    int rc = MP2VG_OK;
+    auto run = [&](size_t i, float* t) -> int {
+        if (pool_install(c, cand[i]) != hipSuccess) return (int)MP2VG_E_HIP;
+        c->last_foot.clear();  // c->stream joined every set (synchronised by pool_install)
+        int r = batch_decode(c);
+        if (r == MP2VG_OK && t) r = mp2vg_batch_times(c, 0, t, nullptr, 0, nullptr);
+        cand[i] = pool_take(c);
+        return r;
+    };
+    const std::vector<uint8_t> tiles0 = c->tiles_ok;
+    for (int w = 0; w < 2 && rc == MP2VG_OK; w++) rc = run(0, nullptr);  // warm-up
+    for (int r = 0; r < 2 && rc == MP2VG_OK; r++)
+        for (size_t i = 0; i < n && rc == MP2VG_OK; i++) {
+            if (r == 0 && i > 0) c->tiles_ok = tiles0;  // a candidate's first decode starts from the batch's entry state
+            rc = run(i, &ms[r * n + i]);
+        }
+    size_t best = 0;
+    if (rc == MP2VG_OK)
+        for (size_t i = 1; i < n; i++)
+            if (std::min(ms[i], ms[n + i]) < std::min(ms[best], ms[n + best])) best = i;
+    for (size_t i = 0; i < n; i++)
+        if (i != best && rc == MP2VG_OK) pool_set_free(cand[i]);
+    if (rc != MP2VG_OK) {  // an error keeps the original pool (its batch status is returned)
+        for (size_t i = 1; i < n; i++) pool_set_free(cand[i]);
+        best = 0;
+    }
+    HIPCHK(pool_install(c, cand[best]));
+    c->place_ms = ms;
+    c->place_kept = rc == MP2VG_OK ? (int)best : -1;
+    if (getenv("MP2VG_TRACE")) {
+        fprintf(stderr, "[mp2vg] placement: %zu candidate pools, batch ms (two rounds)", n);
+        for (float m : ms) fprintf(stderr, " %.3f", m);
+        fprintf(stderr, ", kept %zu\n", best);
+    }
+    return rc;
+}
+
 extern "C" int mp2vg_batch_decode(mp2vg_ctx_t* c) {
     if (!c) return MP2VG_E_INVALID;
     if (!c->batch_ready) {
@@ -982,6 +1146,11 @@ extern "C" int mp2vg_batch_decode(mp2vg_ctx_t* c) {
         return MP2VG_E_STATE;
     }
     HIPCHK(hipSetDevice(c->cfg.device));
+    const int rc = calibrate_placement(c);
+    return rc == 1 ? batch_decode(c) : rc;
+}
+
+static int batch_decode(mp2vg_ctx_t* c) {
     Bank& b = c->bank[c->cur];
     const std::vector<Launch>& launches = b.launches;
     int nl = (int)launches.size();
@@ -1322,6 +1491,14 @@ extern "C" int mp2vg_pool_probe(mp2vg_ctx_t* c, int32_t rw, int32_t reps, double
         return MP2VG_E_HIP;
     }
     *nblocks = (int32_t)c->chunks.size();
+    return MP2VG_OK;
+}
+
+extern "C" int mp2vg_pool_placement(mp2vg_ctx_t* c, float* ms, int32_t max, int32_t* n, int32_t* kept) {
+    if (!c || !n || !kept || max < 0 || (max > 0 && !ms)) return MP2VG_E_INVALID;
+    *n = (int32_t)c->place_ms.size();
+    *kept = c->place_kept;
+    for (int i = 0; i < *n && i < max; i++) ms[i] = c->place_ms[i];
     return MP2VG_OK;
 }
 

@@ -199,6 +199,14 @@ class DeviceContext:
                                      n.value, ctypes.byref(n)), "pool_probe")
         return out
 
+    def placement(self):
+        """The pool placement calibration of this context (mp2vg_pool_placement): (batch ms of
+        each candidate pool, round 0 then round 1; index of the pool kept, -1 if it did not run)."""
+        n, kept = ctypes.c_int32(), ctypes.c_int32()
+        buf = (ctypes.c_float * 16)()
+        check(lib().mp2vg_pool_placement(self.h, buf, 16, ctypes.byref(n), ctypes.byref(kept)), "pool_placement")
+        return [round(float(v), 4) for v in buf[:min(n.value, 16)]], kept.value
+
     def download(self, slot):
         """Visible planes of one slot: [Y, U, V] numpy arrays (height x width)."""
         planes = [np.empty((self.ph[i], self.pw[i]), np.uint8) for i in range(3)]
