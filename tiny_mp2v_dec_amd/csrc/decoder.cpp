@@ -181,6 +181,10 @@ struct Lane {
     PinnedBuf mbuf[2], cbuf[2];        // chunk MB records / coefficient words, one set per record bank
     // frame downloads, slots dealt round-robin: each stream's copies go to their own DMA engine
     hipStream_t dl[kMaxDl] = {};
+    // the host waits for a download stream through one of these (hipEventBlockingSync: the
+    // waiting thread sleeps instead of spinning, which on a CPU-quota'd host costs the parse
+    // workers their share)
+    hipEvent_t dlev[kMaxDl] = {};
     int ndl = 1;
     hipEvent_t decoded = nullptr;      // end of the last chunk's decode (on the context stream)
     int frames = 0;                    // frames decoded in the last decode()
@@ -197,6 +201,8 @@ struct Lane {
         if (ctx) mp2vg_synchronize(ctx);
         dpool.reset();
         if (decoded) hipEventDestroy(decoded);
+        for (hipEvent_t e : dlev)
+            if (e) hipEventDestroy(e);
         for (hipStream_t st : dl)
             if (st) hipStreamDestroy(st);
         if (ctx) mp2vg_destroy(ctx);
@@ -271,7 +277,8 @@ extern "C" int mp2vg_decoder_create_multi(const mp2vg_config_t* cfg, const int32
         L.ndl = kDlStreams;
         bool sok = true;
         for (int k = 0; k < L.ndl; k++)
-            sok = sok && hipStreamCreateWithFlags(&L.dl[k], hipStreamNonBlocking) == hipSuccess;
+            sok = sok && hipStreamCreateWithFlags(&L.dl[k], hipStreamNonBlocking) == hipSuccess &&
+                  hipEventCreateWithFlags(&L.dlev[k], hipEventBlockingSync | hipEventDisableTiming) == hipSuccess;
         if (!sok || hipEventCreateWithFlags(&L.decoded, hipEventDisableTiming) != hipSuccess) {
             set_error("download stream / event creation failed");
             mp2vg_decoder_destroy(d);
@@ -464,8 +471,11 @@ extern "C" int mp2vg_decoder_decode(mp2vg_decoder_t* d, const uint8_t* buf, uint
         if (L.pend.empty()) return MP2VG_OK;
         tc = now_ms();
         hipSetDevice(L.device);
+        static const bool blocking = !getenv("MP2VG_DL_BLOCKING") || atoi(getenv("MP2VG_DL_BLOCKING"));
         for (int i = 0; i < L.ndl; i++)
-            if (hipStreamSynchronize(L.dl[i]) != hipSuccess) return MP2VG_E_HIP;
+            if (blocking ? (hipEventRecord(L.dlev[i], L.dl[i]) != hipSuccess || hipEventSynchronize(L.dlev[i]) != hipSuccess)
+                         : hipStreamSynchronize(L.dl[i]) != hipSuccess)
+                return MP2VG_E_HIP;
         t_down += now_ms() - tc;
         for (auto& kv : L.inflight) ready[kv.first] = kv.second;
         L.inflight.clear();

@@ -258,7 +258,7 @@ extern "C" int mp2vg_create(const mp2vg_config_t* cfg, mp2vg_ctx_t** out) {
     c->nstreams = default_streams(cfg);
     bool ok = true;
     for (Bank& b : c->bank)
-        ok = ok && hipEventCreateWithFlags(&b.uploaded, hipEventDisableTiming) == hipSuccess &&
+        ok = ok && hipEventCreateWithFlags(&b.uploaded, hipEventDisableTiming | hipEventBlockingSync) == hipSuccess &&
              hipEventCreateWithFlags(&b.consumed, hipEventDisableTiming) == hipSuccess;
     if (!ok || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->ustream, hipStreamNonBlocking) != hipSuccess ||

@@ -8,6 +8,7 @@ a slow run's phase.
 """
 import json
 import os
+import resource
 import sys
 import time
 
@@ -30,8 +31,12 @@ for run in range(runs):
         n[0] = 0
         print(f"=== run {run} {'device' if m else 'host'} frames", file=sys.stderr, flush=True)
         t0 = time.perf_counter()
+        r0 = resource.getrusage(resource.RUSAGE_SELF)
         decs[m].decode(es)
         dt = time.perf_counter() - t0
-        print(json.dumps({"run": run, "threads": threads, "device_frames": m, "frames": n[0], "frames_per_s": round(n[0] / dt, 1)}), flush=True)
+        r1 = resource.getrusage(resource.RUSAGE_SELF)
+        cpu = (r1.ru_utime - r0.ru_utime) + (r1.ru_stime - r0.ru_stime)
+        print(json.dumps({"run": run, "threads": threads, "device_frames": m, "frames": n[0],
+                          "frames_per_s": round(n[0] / dt, 1), "cpus_busy": round(cpu / dt, 2)}), flush=True)
 for d in decs.values():
     d.close()
