@@ -155,6 +155,7 @@ struct mp2vg_ctx {
     std::vector<uint8_t> tiles_ok;  // per slot: its tiles match its frame (after the batches enqueued)
     size_t tile_stride = 0;      // 2 x slot bytes, 256-B aligned
     int nstreams = 2;  // independent picture sets per batch (default_streams)
+    int ncu = 0;       // the device's CUs (0 in a host-only planning shell: 256 assumed)
 
     Bank bank[2];
     int cur = -1;  // bank of the last upload
@@ -256,6 +257,7 @@ extern "C" int mp2vg_create(const mp2vg_config_t* cfg, mp2vg_ctx_t** out) {
     c->slot_stride = c->g.slot_bytes + slot_pad();
     c->tile_stride = ((2 * c->g.slot_bytes + 255) & ~(size_t)255) + tile_pad();
     c->nstreams = default_streams(cfg);
+    if (hipDeviceGetAttribute(&c->ncu, hipDeviceAttributeMultiprocessorCount, cfg->device) != hipSuccess) c->ncu = 0;
     bool ok = true;
     for (Bank& b : c->bank)
         ok = ok && hipEventCreateWithFlags(&b.uploaded, hipEventDisableTiming | hipEventBlockingSync) == hipSuccess &&
@@ -749,6 +751,28 @@ static int plan_batch(mp2vg_ctx_t* c, const mp2vg_picture_t* pics, int32_t npics
     // longer workgroups: c5 +1.8 to +6.7 %, three same-box rounds; c1 (4:2:0) no gain)
     static const int rows_i_env = dev_env("MP2VG_SLICE_ROWS_I") ? std::max(1, atoi(dev_env("MP2VG_SLICE_ROWS_I"))) : 0;
     const int rows_i = rows_i_env ? rows_i_env : (c->g.cf == 3 ? 2 : 1);
+    static const int i_split = dev_env("MP2VG_I_SPLIT") ? std::max(1, atoi(dev_env("MP2VG_I_SPLIT"))) : 1;
+    static const int i_mbs = dev_env("MP2VG_I_SLICE_MBS") ? std::max(0, atoi(dev_env("MP2VG_I_SLICE_MBS"))) : 0;
+    // I launches fill whole rounds of resident workgroups: the default slice (rows_i rows), or up
+    // to a quarter more 4-MB groups cut across rows, whichever leaves the launch's last round of
+    // workgroups least empty, against the device's CUs x the I kernel's workgroups per CU (6, or 4
+    // in 4:4:4) shared by the picture sets' concurrent I launches.  (c1: 128-MB slices, 4.98
+    // instead of 5.31 rounds; c5: 256-MB slices, 1.99 instead of 2.13; one-stream I launch -1.5 %
+    // and -3.6 %, profiles/r6/README.md §10.)  A gain under 0.1 round keeps the default.
+    auto i_slice_groups = [&](size_t npic_launch) -> int {
+        const int s0 = rows_i * mbw / 4;
+        if (rows_i_env || i_mbs || i_split > 1 || mbw % 4) return s0;
+        const double cap = (double)(c->ncu > 0 ? c->ncu : 256) * (c->g.cf == 3 ? 4 : 6) / std::max(1, nsets);
+        const double gtot = (double)npic_launch * (mbw / 4) * mbh;
+        auto waste = [&](int sg) {
+            const double r = std::ceil(gtot / sg) / cap;
+            return std::ceil(r) - r;
+        };
+        int best = s0;
+        for (int sg = s0 + 1; sg <= s0 + s0 / 4; sg++)
+            if (waste(sg) < waste(best)) best = sg;
+        return waste(s0) - waste(best) >= 0.1 ? best : s0;
+    };
     for (int set = 0; set < nsets; set++)
     for (int q = 0; q <= maxlevel; q++) {
         std::vector<int> lp;
@@ -812,6 +836,25 @@ static int plan_batch(mp2vg_ctx_t* c, const mp2vg_picture_t* pics, int32_t npics
                             if (k != o) push(k, rr);
                     for (int rr = r; rr < std::min(r + 2, mbh); rr++) push(o, rr);
                 }
+            } else if (types == 1 && mbw % 4 == 0 &&
+                       ((i_mbs > 0 && i_mbs % 4 == 0) || i_slice_groups(lp.size()) != rows_i * mbw / 4)) {
+                // I slices of i_mbs MBs (a multiple of 4: groups never straddle rows; the dev
+                // MP2VG_I_SLICE_MBS, else i_slice_groups), cut across rows, the picture's last
+                // one shorter
+                const int cut = i_mbs > 0 ? i_mbs : 4 * i_slice_groups(lp.size());
+                const int total = mbw * mbh;
+                for (int m0 = 0; m0 < total; m0 += cut)
+                    for (size_t k = i; k < j; k++)
+                        slices.push_back({(uint32_t)lp[k], pics[lp[k]].mb_first + (uint32_t)m0,
+                                          (uint32_t)std::min(cut, total - m0), sflags(lp[k])});
+            } else if (types == 1 && slice_rows == 1 && i_split > 1 && (mbw / i_split) % 4 == 0 && mbw % i_split == 0) {
+                // (dev) I launches in pieces of a row: more, shorter workgroups for the launch tail
+                const int pw = mbw / i_split;
+                for (int r = 0; r < mbh; r++)
+                    for (size_t k = i; k < j; k++)
+                        for (int q = 0; q < i_split; q++)
+                            slices.push_back({(uint32_t)lp[k], pics[lp[k]].mb_first + (uint32_t)(r * mbw + q * pw),
+                                              (uint32_t)pw, sflags(lp[k])});
             } else {
                 for (int r = 0; r < mbh; r += slice_rows)
                     for (size_t k = i; k < j; k++) push(k, r);
