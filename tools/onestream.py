@@ -37,8 +37,9 @@ def main():
     launch_bytes = np.bincount(of_pic, weights=bench.per_picture_bytes(p), minlength=len(modes))
     ctx = R.DeviceContext(w, h, cf, slots=p.npics, one_stream=True)
     ctx.upload(p.pics, p.mbs, p.coefs)
-    ctx.decode()  # warm-up batch (not in the table)
+    ctx.decode()  # warm-up batch (not in the table; with MP2VG_PLACE_ONE_STREAM=1 the placement calibration runs in it)
     ctx.synchronize()
+    place_ms, place_kept = ctx.placement()
     for _ in range(a.reps):
         ctx.decode()
     ctx.synchronize()
@@ -48,6 +49,7 @@ def main():
     exp = bench.expected_digests(a.config, gops, 1729)
     ctx.close()
     out = {"config": a.config, "gops": gops, "frames": int(p.npics), "batches_decoded": a.reps + 1,
+           "pool_placement": {"candidate_batch_ms": place_ms, "kept": place_kept},
            "span_ms": round(span, 4), "parity": None if exp is None else bool(np.array_equal(dig, exp)),
            "per_kernel": {}}
     for m in sorted(set(modes.tolist())):

@@ -28,8 +28,8 @@ def main(d):
             k = kname(r["Kernel_Name"])
             if k:
                 rows[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
-    # per-kernel durations from the kernel trace, without onestream.py's warm-up batch (its first
-    # launches per level): the same launches the tool's HIP-event table averages
+    # per-kernel durations from the kernel trace, the timed batches only (without onestream.py's
+    # warm-up batch and the placement calibration in it): the launches its HIP-event table averages
     stats = {}
     for f in glob.glob(os.path.join(d, "ktrace", "*kernel_trace.csv")):
         disp = sorted((int(r["Correlation_Id"]), kname(r["Kernel_Name"]), int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
@@ -39,7 +39,8 @@ def main(d):
             if line.startswith("{"):
                 ev0 = json.loads(line)
         nl = sum(v["launches_per_batch"] for v in ev0["per_kernel"].values()) if ev0 else 5
-        timed = disp[nl:]
+        reps = ev0["batches_decoded"] - 1 if ev0 else len(disp) // nl - 1
+        timed = disp[-reps * nl:]  # the timed batches are the last ones (placement calibration batches come first)
         by = collections.defaultdict(list)
         for _, k, ns in timed:
             by[k].append(ns / 1e6)
