@@ -203,10 +203,12 @@ int  mp2vg_slot_device_ptr(mp2vg_ctx_t* ctx, int32_t slot, void** dptr);
  * the writes have completed and before mp2vg_batch_decode of a batch that reads the slot. */
 int  mp2vg_invalidate_slot(mp2vg_ctx_t* ctx, int32_t slot);
 /* The pool's placement calibration (runtime.cpp calibrate_placement): at the first batch of a
- * multi-stream context whose pool holds at least MP2VG_PLACE_MIN_MB (4096) MB, the batch is
+ * context whose pool holds at least MP2VG_PLACE_MIN_MB (4096) MB, the batch is
  * decoded on the pool and on MP2VG_PLACE_CANDIDATES - 1 (default 2) copies of it in freshly
  * allocated blocks, and the pool with the shortest batch is kept; every candidate ends in the
- * same state, so no output changes.  MP2VG_PLACE_CANDIDATES=1 turns it off.  This returns the
+ * same state, so no output changes.  The other candidates stay allocated until mp2vg_destroy
+ * while a quarter of the device memory stays free (freeing them slowed the kept pool;
+ * MP2VG_PLACE_HOLD=0 frees them).  MP2VG_PLACE_CANDIDATES=1 turns it off.  This returns the
  * measured batch times (ms[0..n): round 0 of each candidate, then round 1; n = 0 when it did not
  * run) and the candidate kept (0 = the pool as first allocated, -1 = none). */
 int  mp2vg_pool_placement(mp2vg_ctx_t* ctx, float* ms, int32_t max, int32_t* n, int32_t* kept);

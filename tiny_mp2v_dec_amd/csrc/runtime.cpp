@@ -73,6 +73,7 @@ static const char* dev_env(const char* name) {
 #endif
 }
 static void pool_block_free(uint8_t* p, size_t bytes, uint64_t vmm);
+static void free_held_pools(mp2vg_ctx_t* c);
 static size_t slot_pad() {
     const char* e = dev_env("MP2VG_SLOT_PAD");
     return e ? (size_t)std::max(0, atoi(e)) & ~(size_t)255 : 0;
@@ -131,6 +132,7 @@ struct Bank {
     bool decoded = false;           // `consumed` has been recorded
 };
 
+struct PoolSet;
 struct mp2vg_ctx {
     mp2vg_config_t cfg{};
     Geom g{};
@@ -179,6 +181,7 @@ struct mp2vg_ctx {
     bool placed = false;        // the pool's placement was calibrated (calibrate_placement)
     std::vector<float> place_ms;  // its batch times: round 0 of every candidate, then round 1
     int place_kept = -1;          // the candidate kept (0 = the pool as first allocated)
+    std::vector<PoolSet*> place_held;  // the calibration's candidates not kept, held until destroy
 
     void* h_stage = nullptr;
     int32_t* d_dslots = nullptr;
@@ -298,6 +301,7 @@ extern "C" int mp2vg_destroy(mp2vg_ctx_t* c) {
     hipFree(c->d_pool);
     hipFree(c->d_tiles);
     for (size_t i = 0; i < c->chunks.size(); i++) pool_block_free(c->chunks[i], c->chunk_bytes[i], c->chunk_vmm[i]);
+    free_held_pools(c);
     hipFree(c->d_tab);
     hipFree(c->d_sink);
     for (Bank& b : c->bank) {
@@ -1042,6 +1046,14 @@ static void pool_set_free(PoolSet& p) {
     p = PoolSet();
 }
 
+static void free_held_pools(mp2vg_ctx_t* c) {
+    for (PoolSet* p : c->place_held) {
+        pool_set_free(*p);
+        delete p;
+    }
+    c->place_held.clear();
+}
+
 static PoolSet pool_take(mp2vg_ctx_t* c) {
     PoolSet p;
     p.chunks.swap(c->chunks);
@@ -1101,7 +1113,7 @@ static hipError_t pool_clone(mp2vg_ctx_t* c, const PoolSet& src, PoolSet& dst) {
 }
 
 // MP2VG_PLACE_CANDIDATES (pools tried, 1 = off; default 3), MP2VG_PLACE_MIN_MB (smallest pool
-// calibrated; default 4096), MP2VG_PLACE_ONE_STREAM=1 (one-stream contexts too)
+// calibrated; default 4096), MP2VG_PLACE_ONE_STREAM=0 (multi-stream contexts only)
 static int env_int(const char* name, int dflt) {
     const char* e = getenv(name);
     return e && *e ? atoi(e) : dflt;
@@ -1119,9 +1131,7 @@ static int calibrate_placement(mp2vg_ctx_t* c) {
     size_t pool = 0;
     for (size_t b : c->chunk_bytes) pool += b;
     if (k < 2 || c->chunks.empty() || pool < ((size_t)std::max(0, env_int("MP2VG_PLACE_MIN_MB", 4096)) << 20)) return 1;
-    // (a one-stream context is the bench's per-kernel measurement context: calibrated, it ran its
-    // later batches 5 % slower than its calibration runs, a cause not found; off unless asked)
-    if (c->nstreams == 1 && !env_int("MP2VG_PLACE_ONE_STREAM", 0)) return 1;
+    if (c->nstreams == 1 && !env_int("MP2VG_PLACE_ONE_STREAM", 1)) return 1;
     const Bank& bk = c->bank[c->cur];
     std::vector<uint8_t> written(c->nslots, 0);
     for (const auto& w : bk.tiles.writes)
@@ -1165,8 +1175,23 @@ static int calibrate_placement(mp2vg_ctx_t* c) {
     if (rc == MP2VG_OK)
         for (size_t i = 1; i < n; i++)
             if (std::min(ms[i], ms[n + i]) < std::min(ms[best], ms[n + best])) best = i;
+    // The candidates not kept stay allocated until the context is destroyed: freeing them made
+    // the kept pool's later batches 8 % slower for good (one-stream c2: 8.67-8.70 ms per batch
+    // after the calibration measured it at 7.9-8.0, and still after a 10-s pause; held: 7.97; the
+    // bench step: freed 380.7-383.3k, held 389.7-391.7k, uncalibrated 387.9-388.0k frames/s,
+    // profiles/r6/README.md §11).  Held while a quarter of the device stays free
+    // (MP2VG_PLACE_HOLD=0 frees them, =1 holds them regardless).
+    size_t free_now = 0, total_now = 0;
+    const bool room = hipMemGetInfo(&free_now, &total_now) == hipSuccess && free_now >= total_now / 4;
+    const int hold_env = env_int("MP2VG_PLACE_HOLD", -1);
+    const bool hold = hold_env < 0 ? room : hold_env != 0;
     for (size_t i = 0; i < n; i++)
-        if (i != best && rc == MP2VG_OK) pool_set_free(cand[i]);
+        if (i != best && rc == MP2VG_OK) {
+            if (hold)
+                c->place_held.push_back(new PoolSet(std::move(cand[i])));
+            else
+                pool_set_free(cand[i]);
+        }
     if (rc != MP2VG_OK) {  // an error keeps the original pool (its batch status is returned)
         for (size_t i = 1; i < n; i++) pool_set_free(cand[i]);
         best = 0;
@@ -1175,7 +1200,8 @@ static int calibrate_placement(mp2vg_ctx_t* c) {
     c->place_ms = ms;
     c->place_kept = rc == MP2VG_OK ? (int)best : -1;
     if (getenv("MP2VG_TRACE")) {
-        fprintf(stderr, "[mp2vg] placement: %zu candidate pools, batch ms (two rounds)", n);
+        fprintf(stderr, "[mp2vg] placement: %zu candidate pools (others %s), batch ms (two rounds)", n,
+                hold ? "held" : "freed");
         for (float m : ms) fprintf(stderr, " %.3f", m);
         fprintf(stderr, ", kept %zu\n", best);
     }

@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--config", default="c2")
     ap.add_argument("--gops", type=int, default=None)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--sleep", type=float, default=0.0, help="host seconds between the warm-up batch and the timed ones")
     a = ap.parse_args()
     w, h, cf, extra, _ = bench.CONFIGS[a.config]
     gops = a.gops or bench.DEFAULT_GOPS[a.config]
@@ -40,6 +41,9 @@ def main():
     ctx.decode()  # warm-up batch (not in the table; with MP2VG_PLACE_ONE_STREAM=1 the placement calibration runs in it)
     ctx.synchronize()
     place_ms, place_kept = ctx.placement()
+    if a.sleep > 0:
+        import time
+        time.sleep(a.sleep)
     for _ in range(a.reps):
         ctx.decode()
     ctx.synchronize()
