@@ -1157,7 +1157,10 @@ static int calibrate_placement(mp2vg_ctx_t* c) {
     std::vector<float> ms(2 * n, 0.f);
     int rc = MP2VG_OK;
     auto run = [&](size_t i, float* t) -> int {
-        if (pool_install(c, cand[i]) != hipSuccess) return (int)MP2VG_E_HIP;
+        if (pool_install(c, cand[i]) != hipSuccess) {
+            cand[i] = pool_take(c);  // (the pool goes back to its candidate slot either way)
+            return (int)MP2VG_E_HIP;
+        }
         c->last_foot.clear();  // c->stream joined every set (synchronised by pool_install)
         int r = batch_decode(c);
         if (r == MP2VG_OK && t) r = mp2vg_batch_times(c, 0, t, nullptr, 0, nullptr);
