@@ -195,7 +195,10 @@ int  mp2vg_copy_slot_packed(mp2vg_ctx_t* ctx, int32_t slot, void* dst, int32_t d
  * slot is READ-ONLY for callers: the motion-compensation taps read a reference from its anchor
  * tiles, a second copy the decode writes next to the frame (recon.hip), so bytes written through
  * this pointer are not seen by later predictions unless the caller then calls
- * mp2vg_invalidate_slot, which makes the next decode that reads the slot rebuild its tiles. */
+ * mp2vg_invalidate_slot, which makes the next decode that reads the slot rebuild its tiles.
+ * The pointer can change once, at the context's first mp2vg_batch_decode, when the pool's
+ * placement calibration keeps a copy of the pool (mp2vg_pool_placement; contents are carried
+ * over): fetch it after that decode, or turn the calibration off (MP2VG_PLACE_CANDIDATES=1). */
 int  mp2vg_slot_device_ptr(mp2vg_ctx_t* ctx, int32_t slot, void** dptr);
 /* the slot's frame was written by someone other than the decode (an RCCL receive, an external
  * producer writing through mp2vg_slot_device_ptr): its anchor tiles are stale.  The next batch
