@@ -12,6 +12,7 @@
 //                     a frame valid only for the duration of the call.
 //   decode() returns after every frame has been rendered (reference flush/kill semantics,
 //   decoder.cpp:244-254 + threads.cpp:198-211).
+#include <pthread.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -222,6 +223,10 @@ struct mp2vg_decoder {
     // device it was allocated under; lanes on several devices copy by DMA)
     bool kernel_copy = false;
     mp2vg_stream_headers_t hdrs{};     // of the last decode()
+    // the CPUs of the first device's NUMA node (its PCI local_cpulist) that the process may use:
+    // with MP2VG_PIN=1 decode()'s threads run there
+    bool pin = false;
+    cpu_set_t local{};
     // of the last decode(): lane changes that found the lane just left still downloading (its
     // chunk left in flight, the host moving on), and host blocks on another lane's downloads
     // (only when the frame pool runs short); lane changes whose lane just left had nothing in
@@ -253,6 +258,13 @@ extern "C" int mp2vg_decoder_create_multi(const mp2vg_config_t* cfg, const int32
     d->user = user;
     d->g.init(cfg->width, cfg->height, cfg->chroma_format);
     d->device_frames = cfg->reserved & MP2VG_DECODER_DEVICE_FRAMES;
+    // (opt-in, MP2VG_PIN=1: on a shared 2-socket host it did not steady the slow decode() calls,
+    // profiles/r6/dropin_pin_ab.txt)
+    if (getenv("MP2VG_PIN") && atoi(getenv("MP2VG_PIN"))) {
+        char bus[64] = {0};
+        d->pin = hipDeviceGetPCIBusId(bus, (int)sizeof(bus), devices[0]) == hipSuccess &&
+                 device_local_cpus(bus, &d->local);
+    }
     // the copy kernel: into pinned host frames (one device), or into each lane's own HBM frames
     d->kernel_copy = kDlKernel;
     for (int i = 1; i < ndevices; i++) d->kernel_copy = d->kernel_copy && (d->device_frames || devices[i] == devices[0]);
@@ -348,8 +360,31 @@ extern "C" int mp2vg_decoder_frames_allocated(const mp2vg_decoder_t* d) {
     return (int)n;
 }
 
+// Runs decode() with the calling thread on the decoder's NUMA-local CPUs: the parse workers and
+// the render thread it starts inherit them, the parallel_for helpers are moved there; the caller's
+// own affinity comes back on return.
+struct LocalCpus {
+    bool on = false;
+    cpu_set_t saved{};
+    explicit LocalCpus(const mp2vg_decoder_t* d) {
+        if (!d->pin || pthread_getaffinity_np(pthread_self(), sizeof(saved), &saved) != 0) return;
+        on = pthread_setaffinity_np(pthread_self(), sizeof(d->local), &d->local) == 0;
+        if (on) parallel_for_pin(d->local);
+    }
+    ~LocalCpus() {
+        if (on) pthread_setaffinity_np(pthread_self(), sizeof(saved), &saved);
+    }
+};
+
+static int decoder_decode(mp2vg_decoder_t* d, const uint8_t* buf, uint64_t len);
+
 extern "C" int mp2vg_decoder_decode(mp2vg_decoder_t* d, const uint8_t* buf, uint64_t len) {
     if (!d || !buf) return MP2VG_E_INVALID;
+    LocalCpus guard(d);
+    return decoder_decode(d, buf, len);
+}
+
+static int decoder_decode(mp2vg_decoder_t* d, const uint8_t* buf, uint64_t len) {
     // the parse runs on worker threads while the chunks below go through the device: a chunk
     // waits only for its own pictures (one thread is left for this loop; the renderer mostly
     // waits on downloads)

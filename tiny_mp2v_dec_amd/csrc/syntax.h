@@ -3,6 +3,7 @@
 // reference's parse semantics both must agree on (qscale mapping, MV prediction, W build, MC
 // read extents).
 #pragma once
+#include <sched.h>
 #include <cstdint>
 #include <cstring>
 #include <functional>
@@ -331,6 +332,11 @@ void parallel_for(int n, int max_threads, const std::function<void(int)>& fn);
 // cgroup v2 CPU quota (cpu.max "quota period": a container allowed 16 CPUs' time on a 256-CPU host
 // is throttled for the rest of each period once its threads have used it) (tables.cpp)
 int cpu_budget();
+
+// The CPUs local to a PCI device (sysfs local_cpulist: its NUMA node) that this process may use;
+// false when unknown.  parallel_for_pin restricts the parallel_for helper threads to a set.
+bool device_local_cpus(const char* pci_bus_id, cpu_set_t* out);
+void parallel_for_pin(const cpu_set_t& set);
 
 // Host phase timing for diagnosis: with MP2VG_TRACE set, trace_phase(name, t0) prints the
 // milliseconds since t0 to stderr and returns the current time.

@@ -1,5 +1,7 @@
+#include <pthread.h>
 #include <sched.h>
 
+#include <cctype>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -144,6 +146,9 @@ class HelperPool {
         for (auto& t : th_) t.join();
     }
     int size() const { return (int)th_.size(); }
+    void pin(const cpu_set_t& set) {
+        for (auto& t : th_) pthread_setaffinity_np(t.native_handle(), sizeof(set), &set);
+    }
     void run(int n, int helpers, const std::function<void(int)>& fn) {
         std::lock_guard<std::mutex> call(call_mu_);
         {
@@ -211,9 +216,42 @@ int cpu_budget() {
     return budget;
 }
 
+static HelperPool* helper_pool() {
+    static HelperPool* pool = new HelperPool(std::max(0, std::min(15, cpu_budget() - 1)));  // never destroyed
+    return pool;
+}
+
+void parallel_for_pin(const cpu_set_t& set) { helper_pool()->pin(set); }
+
+bool device_local_cpus(const char* pci_bus_id, cpu_set_t* out) {
+    std::string id(pci_bus_id);
+    for (auto& ch : id) ch = (char)tolower((unsigned char)ch);
+    FILE* f = fopen(("/sys/bus/pci/devices/" + id + "/local_cpulist").c_str(), "r");
+    if (!f) return false;
+    char buf[4096] = {0};
+    const bool got = fgets(buf, sizeof(buf), f) != nullptr;
+    fclose(f);
+    if (!got) return false;
+    cpu_set_t allowed, set;
+    CPU_ZERO(&set);
+    if (sched_getaffinity(0, sizeof(allowed), &allowed) != 0) return false;
+    for (char* p = buf; *p && *p != '\n';) {  // "0-63,128-191"
+        char* e;
+        long a = strtol(p, &e, 10), b = a;
+        if (e == p) break;
+        if (*e == '-') b = strtol(e + 1, &e, 10);
+        for (long c = a; c <= b && c < CPU_SETSIZE; c++)
+            if (c >= 0 && CPU_ISSET(c, &allowed)) CPU_SET(c, &set);
+        p = *e == ',' ? e + 1 : e;
+    }
+    if (CPU_COUNT(&set) == 0) return false;
+    *out = set;
+    return true;
+}
+
 void parallel_for(int n, int max_threads, const std::function<void(int)>& fn) {
     if (n <= 0) return;
-    static HelperPool* pool = new HelperPool(std::max(0, std::min(15, cpu_budget() - 1)));  // never destroyed
+    HelperPool* pool = helper_pool();
     const int helpers = std::min({max_threads - 1, pool->size(), n - 1});
     if (helpers <= 0) {
         for (int i = 0; i < n; i++) fn(i);
