@@ -210,7 +210,7 @@ int  mp2vg_invalidate_slot(mp2vg_ctx_t* ctx, int32_t slot);
  * decoded on the pool and on MP2VG_PLACE_CANDIDATES - 1 (default 2) copies of it in freshly
  * allocated blocks, and the pool with the shortest batch is kept; every candidate ends in the
  * same state, so no output changes.  The other candidates stay allocated until mp2vg_destroy
- * while a quarter of the device memory stays free (freeing them slowed the kept pool;
+ * while an eighth of the device memory stays free (freeing them slowed the kept pool;
  * MP2VG_PLACE_HOLD=0 frees them).  MP2VG_PLACE_CANDIDATES=1 turns it off.  This returns the
  * measured batch times (ms[0..n): round 0 of each candidate, then round 1; n = 0 when it did not
  * run) and the candidate kept (0 = the pool as first allocated, -1 = none). */

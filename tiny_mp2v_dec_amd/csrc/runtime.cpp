@@ -1182,10 +1182,11 @@ static int calibrate_placement(mp2vg_ctx_t* c) {
     // the kept pool's later batches 8 % slower for good (one-stream c2: 8.67-8.70 ms per batch
     // after the calibration measured it at 7.9-8.0, and still after a 10-s pause; held: 7.97; the
     // bench step: freed 380.7-383.3k, held 389.7-391.7k, uncalibrated 387.9-388.0k frames/s,
-    // profiles/r6/README.md §11).  Held while a quarter of the device stays free
-    // (MP2VG_PLACE_HOLD=0 frees them, =1 holds them regardless).
+    // profiles/r6/README.md §11).  Held while an eighth of the device stays free (c3's bench holds
+    // both its contexts' candidates: 231 of 288 GB; MP2VG_PLACE_HOLD=0 frees them, =1 holds them
+    // regardless).
     size_t free_now = 0, total_now = 0;
-    const bool room = hipMemGetInfo(&free_now, &total_now) == hipSuccess && free_now >= total_now / 4;
+    const bool room = hipMemGetInfo(&free_now, &total_now) == hipSuccess && free_now >= total_now / 8;
     const int hold_env = env_int("MP2VG_PLACE_HOLD", -1);
     const bool hold = hold_env < 0 ? room : hold_env != 0;
     for (size_t i = 0; i < n; i++)
