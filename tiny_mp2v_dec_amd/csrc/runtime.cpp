@@ -1112,7 +1112,7 @@ static hipError_t pool_clone(mp2vg_ctx_t* c, const PoolSet& src, PoolSet& dst) {
     return hipStreamSynchronize(c->stream);
 }
 
-// MP2VG_PLACE_CANDIDATES (pools tried, 1 = off; default 3), MP2VG_PLACE_MIN_MB (smallest pool
+// MP2VG_PLACE_CANDIDATES (pools tried, 1 = off; default 3, at most 6), MP2VG_PLACE_MIN_MB (smallest pool
 // calibrated; default 4096), MP2VG_PLACE_ONE_STREAM=0 (multi-stream contexts only)
 static int env_int(const char* name, int dflt) {
     const char* e = getenv(name);
@@ -1127,7 +1127,7 @@ static int env_int(const char* name, int dflt) {
 // before the batch (TilePlan.ext_reads); other batches are decoded once, uncalibrated.
 static int calibrate_placement(mp2vg_ctx_t* c) {
     if (c->placed) return 1;
-    const int k = std::max(1, std::min(4, env_int("MP2VG_PLACE_CANDIDATES", 3)));
+    const int k = std::max(1, std::min(6, env_int("MP2VG_PLACE_CANDIDATES", 3)));
     size_t pool = 0;
     for (size_t b : c->chunk_bytes) pool += b;
     if (k < 2 || c->chunks.empty() || pool < ((size_t)std::max(0, env_int("MP2VG_PLACE_MIN_MB", 4096)) << 20)) return 1;
@@ -1144,8 +1144,10 @@ static int calibrate_placement(mp2vg_ctx_t* c) {
     HIPCHK(hipStreamSynchronize(c->stream));
     std::vector<PoolSet> cand;
     cand.push_back(pool_take(c));
-    // (candidates only while the device keeps 8 GB free beside them)
-    for (int i = 1; i < k && free_b > (size_t)i * pool + ((size_t)8 << 30); i++) {
+    // candidates only while an eighth of the device (at least 8 GB) stays free beside them, so
+    // that the ones not kept can be held (below)
+    const size_t reserve = std::max(total_b / 8, (size_t)8 << 30);
+    for (int i = 1; i < k && free_b >= (size_t)i * pool + reserve; i++) {
         PoolSet p;
         if (pool_clone(c, cand[0], p) != hipSuccess) {
             (void)hipGetLastError();
