@@ -29,6 +29,8 @@ def main():
     ap.add_argument("--gops", type=int, default=None)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--sleep", type=float, default=0.0, help="host seconds between the warm-up batch and the timed ones")
+    ap.add_argument("--ballast-after-gb", type=float, default=0.0,
+                    help="device memory allocated (and touched) after the context's pool, held to the end")
     a = ap.parse_args()
     w, h, cf, extra, _ = bench.CONFIGS[a.config]
     gops = a.gops or bench.DEFAULT_GOPS[a.config]
@@ -38,6 +40,12 @@ def main():
     launch_bytes = np.bincount(of_pic, weights=bench.per_picture_bytes(p), minlength=len(modes))
     ctx = R.DeviceContext(w, h, cf, slots=p.npics, one_stream=True)
     ctx.upload(p.pics, p.mbs, p.coefs)
+    if a.ballast_after_gb > 0:
+        import ctypes
+        hip = ctypes.CDLL("libamdhip64.so")
+        ballast = ctypes.c_void_p()
+        nb = ctypes.c_size_t(int(a.ballast_after_gb * (1 << 30)))
+        assert hip.hipMalloc(ctypes.byref(ballast), nb) == 0 and hip.hipMemset(ballast, 0, nb) == 0
     ctx.decode()  # warm-up batch (not in the table; with MP2VG_PLACE_ONE_STREAM=1 the placement calibration runs in it)
     ctx.synchronize()
     place_ms, place_kept = ctx.placement()
