@@ -14,6 +14,8 @@
 //   E  prediction (cascaded half-pel with v_lerp_u8 == _mm_avg_epu8, bidir average) + residual
 //      with clamp (packed i16) and one 16-B / 8-B store per row
 #include <hip/hip_runtime.h>
+
+#include <cstdlib>
 #include <stdint.h>
 #include <stdlib.h>
 
@@ -1720,7 +1722,8 @@ hipError_t launch_frame_copy(const FrameCopy& fc, int n, uint64_t bytes, hipStre
         if (((uintptr_t)fc.src[i] | (uintptr_t)fc.dst[i]) & 15) return hipErrorInvalidValue;
     // about 64 workgroups per launch: PCIe-bound, so few waves; the rest of the chip stays with
     // the next chunk's decode
-    dim3 block(256), grid(n < 64 ? 64 / n : 1, n);
+    static const int wgs = getenv("MP2VG_DL_WGS") ? std::max(1, atoi(getenv("MP2VG_DL_WGS"))) : 64;  // (measurements)
+    dim3 block(256), grid(n < wgs ? wgs / n : 1, n);
     hipLaunchKernelGGL(frame_copy_kernel, grid, block, 0, stream, fc, bytes);
     return hipGetLastError();
 }
