@@ -222,6 +222,9 @@ int  mp2vg_sink_device_ptr(mp2vg_ctx_t* ctx, void** dptr);
 /* diagnostics: the device's shader clock (GHz) while every SIMD issues VALU for ~1 ms (s_memtime
  * against the 100-MHz s_memrealtime); bench.py records it per box.  Synchronises the device. */
 int  mp2vg_clock_probe(int32_t device, double* ghz);
+/* the host threads a decoder uses when num_threads = 0: the hardware threads, capped by the
+ * process's affinity mask and a cgroup v2 CPU quota (cpu.max); no device needed */
+int  mp2vg_cpu_budget(void);
 /* diagnostics (pool placement, tools/placement.py): per pool block (frames and tiles of 16 slots
  * each, in allocation order: frames, tiles, frames, ...) the HBM rate in GB/s of `reps` sweeps
  * that load every 16-B word and, with rw = 1, store it back unchanged.  gbps[i] for the first

@@ -87,3 +87,17 @@ def test_no_silent_cpu_fallback_without_gpu():
     h = ctypes.c_void_p()
     rc = _lib.lib().mp2vg_create(ctypes.byref(cfg), ctypes.byref(h))
     assert rc == -3  # MP2VG_E_HIP
+
+
+def test_cpu_budget_within_the_process_cpus():
+    """mp2vg_cpu_budget (the decoder's default thread count): at least 1, at most the CPUs this
+    process may run on, and at most a cgroup v2 cpu.max quota when one is set."""
+    import os
+    n = _lib.lib().mp2vg_cpu_budget()
+    assert 1 <= n <= len(os.sched_getaffinity(0))
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            assert n <= max(1, int(q) // int(period))
+    except (OSError, ValueError):
+        pass

@@ -109,7 +109,7 @@ RENDER_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.POINTER(Frame))
 EXPORTS = [
     "mp2vg_abi_version", "mp2vg_status_string", "mp2vg_last_error", "mp2vg_create", "mp2vg_destroy",
     "mp2vg_frame_geometry", "mp2vg_reserve_slots", "mp2vg_batch_upload", "mp2vg_batch_validate", "mp2vg_batch_decode",
-    "mp2vg_synchronize", "mp2vg_last_launch_times", "mp2vg_last_batch_time", "mp2vg_batch_times", "mp2vg_batches_span", "mp2vg_download_slot", "mp2vg_copy_slot_packed", "mp2vg_slot_device_ptr", "mp2vg_sink_device_ptr", "mp2vg_clock_probe", "mp2vg_pool_probe", "mp2vg_pool_placement", "mp2vg_invalidate_slot",
+    "mp2vg_synchronize", "mp2vg_last_launch_times", "mp2vg_last_batch_time", "mp2vg_batch_times", "mp2vg_batches_span", "mp2vg_download_slot", "mp2vg_copy_slot_packed", "mp2vg_slot_device_ptr", "mp2vg_sink_device_ptr", "mp2vg_clock_probe", "mp2vg_pool_probe", "mp2vg_pool_placement", "mp2vg_cpu_budget", "mp2vg_invalidate_slot",
     "mp2vg_slot_digests", "mp2vg_parse_es", "mp2vg_parsed_counts", "mp2vg_parsed_pictures", "mp2vg_parsed_mbs",
     "mp2vg_parsed_coefs", "mp2vg_parsed_display_order", "mp2vg_parsed_gop_index", "mp2vg_parsed_stream_headers",
     "mp2vg_parsed_shards", "mp2vg_parsed_free", "mp2vg_vlc_decode",
@@ -155,6 +155,7 @@ def lib():
         "mp2vg_clock_probe": ([I32, P(ctypes.c_double)], ctypes.c_int),
         "mp2vg_pool_probe": ([VP, I32, I32, P(ctypes.c_double), I32, P(I32)], ctypes.c_int),
         "mp2vg_pool_placement": ([VP, P(ctypes.c_float), I32, P(I32), P(I32)], ctypes.c_int),
+        "mp2vg_cpu_budget": ([], ctypes.c_int),
         "mp2vg_invalidate_slot": ([VP, I32], ctypes.c_int),
         "mp2vg_slot_digests": ([VP, P(I32), I32, P(ctypes.c_uint64)], ctypes.c_int),
         "mp2vg_parse_es": ([VP, U64, P(Config), P(VP)], ctypes.c_int),

@@ -269,6 +269,8 @@ extern "C" {
 
 int mp2vg_abi_version(void) { return MP2VG_ABI_VERSION; }
 
+int mp2vg_cpu_budget(void) { return mp2vg::cpu_budget(); }
+
 const char* mp2vg_last_error(void) { return mp2vg::g_last_error.c_str(); }
 
 const char* mp2vg_status_string(int s) {
