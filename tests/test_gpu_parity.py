@@ -526,3 +526,24 @@ def test_pool_placement_calibration_keeps_every_frame(monkeypatch):
             got = ctx.download(p)
             for k in range(3):
                 assert np.array_equal(got[k], exp[p][k]), (p, k)
+
+
+@pytest.mark.parametrize("config,gops", [("c1", 120), ("c5", 64)])
+def test_whole_round_i_slices_vs_reference_digests(config, gops):
+    """The I-only bench batches at their bench sizes, where the planner cuts I slices across MB
+    rows to fill whole rounds of resident workgroups (runtime.cpp i_slice_groups: c1 128-MB, c5
+    256-MB slices): every frame's device digest == the compiled reference's
+    (tests/golden/bench_digests.npz)."""
+    import importlib
+    bench = importlib.import_module("bench")
+    width, height, cf, gparams, _ = bench.CONFIGS[config]
+    es = R.generate_es(width=width, height=height, chroma_format=cf, n_gops=gops, seed=1729, **gparams)
+    parsed = R.Parsed(es, width, height, cf, threads=8)
+    exp = bench.expected_digests(config, gops, 1729)
+    assert exp is not None
+    with R.DeviceContext(width, height, cf, slots=parsed.npics) as ctx:
+        ctx.upload(parsed.pics, parsed.mbs, parsed.coefs)
+        ctx.decode()
+        ctx.synchronize()
+        dig = ctx.digests(np.arange(parsed.npics))
+    assert np.array_equal(dig, exp)
