@@ -1017,8 +1017,12 @@ __device__ __forceinline__ void dequant_word(LT& L, int wave, uint32_t w, uint32
         const int v = min(max((int)(short)val, -2048), 2047);  // int16 truncation (:146), v_med3_i32
         short o;
         if constexpr (LT::WB) {
-            const int dcm = (int)(w << 1) >> 31;  // DC word (bit 30): the value itself
-            o = (short)((level & dcm) | (v & ~dcm));
+            // DC word (bit 30): the value itself -- one sign-extended bit field and one bit-field
+            // insert (the compiler's select was and + cmp + cndmask)
+            const uint32_t dcm = (uint32_t)__builtin_amdgcn_sbfe((int)w, 30, 1);
+            uint32_t ov;
+            asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(ov) : "v"(dcm), "v"(w), "v"((uint32_t)v));
+            o = (short)ov;
         } else {
             o = (w & MP2VG_COEF_DC) ? (short)level : (short)v;
         }
