@@ -875,7 +875,8 @@ struct Lds {
     uint8_t Wb[WB && CF != 1 ? Fmt<CF>::NB : 0][64];  // zero-length (clang extension) when unused: no layout change
     // I kernels (MP2VG_I_KBTAB): per coefficient word's (MB in group k, block b) = bits 22-27, the
     // block's byte address in the wave's blocks with its XOR chunk base, slot * 128 | (slot & 7) * 16
-    // (bits 0-15), and k * 8, the bit offset of MB k's quantiser scale in qs8 (bits 16-20): one LDS
+    // (bits 8-23), and k * 8, the bit offset of MB k's quantiser scale in qs8 (bits 0-4, which is
+    // what v_bfe_u32 reads of its offset operand: no shift per word): one LDS
     // read in place of the slot arithmetic (bfe, bfe, mad, three shifts, bitop3, add3) per word
     // round.  Last in the layout: c5 is sensitive to where the small tables above sit.
     uint32_t kbtab[WB ? 64 : 0];
@@ -1008,7 +1009,8 @@ __device__ __forceinline__ void dequant_word(LT& L, int wave, uint32_t w, uint32
                                : (LT::WB ? ((const uint8_t*)L.Wb)[(w >> 16) & 0x3ffu] : L.W[4 * h + (b < 6 ? 0 : 2)][i]);
         uint32_t kb = 0;  // the (k, b) table entry (MP2VG_I_KBTAB)
         if constexpr (LT::WB && MP2VG_I_KBTAB) kb = L.kbtab[(w >> 22) & 63u];
-        const uint32_t qsk = (LT::WB && MP2VG_I_KBTAB) ? __builtin_amdgcn_ubfe(qs8, kb >> 16, 8) : pick8(qs8, (int)k);
+        // (v_bfe_u32 reads its offset's low 5 bits: the entry's k * 8)
+        const uint32_t qsk = (LT::WB && MP2VG_I_KBTAB) ? __builtin_amdgcn_ubfe(qs8, kb, 8) : pick8(qs8, (int)k);
         const uint32_t wq = __umul24((uint32_t)Wi, qsk);
         // (|level| * W * qs) >> 4 with the sign applied after the shift (truncation toward zero):
         // the signed product, biased by 15 when negative, then an arithmetic shift
@@ -1031,7 +1033,7 @@ __device__ __forceinline__ void dequant_word(LT& L, int wave, uint32_t w, uint32
         if constexpr (LT::WB) {
             // byte address: slot * 128 + ((slot & 7) * 16 XOR doubled scan position)
             const uint32_t a = MP2VG_I_KBTAB
-                                   ? (uint32_t)(uintptr_t)(lds_short2_t*)L.blk[wave] + ((kb & 0xffffu) ^ (uint32_t)L.scan[64 * h + i])
+                                   ? (uint32_t)(uintptr_t)(lds_short2_t*)L.blk[wave] + ((kb >> 8) ^ (uint32_t)L.scan[64 * h + i])
                                    : (uint32_t)(uintptr_t)(lds_short2_t*)L.blk[wave] + ((uint32_t)slot << 7) +
                                          ((((uint32_t)slot << 4) & 0x70u) ^ (uint32_t)L.scan[64 * h + i]);
             const uint32_t d = (uint32_t)(uintptr_t)(lds_short2_t*)L.res[wave];
@@ -1490,7 +1492,7 @@ __global__ __launch_bounds__((64 * kernel_waves<MCM, ABL>())) __attribute__((amd
         if constexpr (LT::WB && MP2VG_I_KBTAB) {
             const int k = lane >> 4, bb = lane & 15;
             const uint32_t slot = (uint32_t)(k * Fmt<CF>::NB + (bb < Fmt<CF>::NB ? bb : 0));
-            L.kbtab[lane] = ((slot << 7) | ((slot << 4) & 0x70u)) | ((uint32_t)k * 8u << 16);
+            L.kbtab[lane] = (((slot << 7) | ((slot << 4) & 0x70u)) << 8) | ((uint32_t)k * 8u);
         }
         if constexpr (LT::WB && CF != 1) {
 #pragma unroll
